@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""bench.py -- pileup sites/sec of the MI355X somatic scorer (BASELINE.json metric).
+
+One STEP = one pass of the scoring path (ss_score_batch_device: main + deep +
+giant kernels) over one HBM-resident batch of synthetic 60xT/30xN pileup sites
+(Poisson depths).  Inputs are generated on the device before
+timing; the timed region contains only scoring.
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL backend only for the
+barrier and the max-over-ranks timing reduction).  Each rank scores its own
+genome shard (synth shard = rank) -- no collective on the data path, weak
+scaling.  value = sites scored by all ranks / max rank time.
+
+Extra fields: "roofline" (main kernel, HIP events over the timed region,
+algorithmic bytes 4 B/read + 16 B/site) and "cpu_baseline" (the real reference
+glf_somatic compiled from source, oracle/_ref/ref_harness, 1 core, rank 0 at
+N=1 only, on a bounded sample of the same synthetic workload, also used as a
+parity spot check).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def cpu_baseline(lt, ln, sample, seed, gpu_scores_prefix):
+    """Time the reference's glf_somatic (compiled from /root/reference) on `sample`
+    sites of shard 0; falls back to the CPU port when the binary is absent."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    scores_path = os.path.join("/tmp", f"ss_cpu_scores_{os.getpid()}.bin")
+    if os.path.exists(harness):
+        out = subprocess.run([harness, "synth", str(lt), str(ln), str(sample), "--seed", str(seed),
+                              "--shard", "0", "--scores", scores_path],
+                             check=True, capture_output=True, text=True).stdout
+        r = json.loads(out.strip().splitlines()[-1])
+        kind, value = "reference", r["sites_per_s"]
+        cpu_scores = np.fromfile(scores_path, np.int32)
+        os.unlink(scores_path)
+        desc = (f"{sample} synthetic sites ({lt}xT/{ln}xN, shard 0, first sites of step batch 0), "
+                f"reference glf_somatic only (pileups prebuilt, BAM decode excluded), 1 thread")
+    else:
+        from __graft_entry__ import load_package
+        from oracle import binding as ob
+        pkg = load_package()
+        h = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=seed), 0, sample)
+        o = ob.Oracle()
+        t0 = time.perf_counter()
+        cpu_scores, _, _ = o.score_batch(h.ref, h.off_tumor, h.off_normal, h.reads_tumor,
+                                         h.reads_normal, want_glf=False)
+        dt = time.perf_counter() - t0
+        kind, value = "port", sample / dt
+        desc = f"{sample} synthetic sites ({lt}xT/{ln}xN), CPU restatement oracle, 1 thread"
+    parity = None
+    if gpu_scores_prefix is not None and len(gpu_scores_prefix) >= sample:
+        parity = bool((gpu_scores_prefix[:sample] == cpu_scores).all())
+    return {"value": round(value, 1), "unit": "sites/s", "cores": 1, "kind": kind,
+            "sample": desc, "parity_vs_gpu": parity}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sites", type=int, default=1 << 24, help="sites per batch (per step, per GPU)")
+    ap.add_argument("--batches", type=int, default=2, help="distinct resident batches cycled per rank")
+    ap.add_argument("--lt", type=float, default=60.0)
+    ap.add_argument("--ln", type=float, default=30.0)
+    ap.add_argument("--seed", type=int, default=0x5EED5A1DC0FFEE01)
+    ap.add_argument("--cpu-sample", type=int, default=2_000_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    ctx = pkg.Context(pkg.Params.default(), device=local)
+
+    # ---- resident synthetic batches (this rank's shard) ----
+    S = args.sites
+    batches = []
+    for b in range(args.batches):
+        syn = pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=rank)
+        d = ctx.synth_device(syn, b * S, S, device=dev)
+        batches.append(d)
+    torch.cuda.synchronize(dev)
+    reads = [sum(d["n_reads"]) for d in batches]
+    bytes_per_batch = [4 * r + 16 * S for r in reads]
+    score = [torch.empty(S, dtype=torch.int32, device=dev) for _ in batches]
+    cap = max(1024, S // 256)
+    calls = torch.zeros(cap * 28, dtype=torch.uint8, device=dev)
+    ncalls = torch.zeros(1, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i):
+        k = i % len(batches)
+        d = batches[k]
+        ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"],
+                         d["reads_normal"], score=score[k], calls=calls, calls_cap=cap,
+                         n_calls=ncalls, stream=stream)
+        return k
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    ctx.check()
+
+    # ---- timed region ----
+    ctx.set_kernel_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    used = []
+    for i in range(args.steps):
+        used.append(step(i))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.set_kernel_timing(False)
+    ctx.check()
+    elapsed = t1 - t0
+    kms = ctx.kernel_time_log()
+    sites_rank = S * args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        s = torch.tensor([sites_rank], dtype=torch.float64, device=dev)
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        total_sites = float(s.item())
+    else:
+        total_sites = float(sites_rank)
+
+    avg_kernel_ms = float(np.mean(kms)) if len(kms) else None
+    alg_bytes = float(np.mean([bytes_per_batch[k] for k in used]))
+    achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms else None
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("sites") == S and tj.get("lt") == args.lt and tj.get("ln") == args.ln:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": "pileup sites/sec at 60xT/30xN (1->8 GPU scaling; achieved HBM GB/s vs roofline)",
+        "value": round(total_sites / elapsed, 1),
+        "unit": "sites/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32+f64 (u32 packed reads)",
+        "data": "synthetic (device-generated counter-based pileups, Poisson depth)",
+        "config": {"workload": f"synthetic WGS shard per GPU, {args.lt:g}xT/{args.ln:g}xN Poisson depth",
+                   "sites_per_step_per_gpu": S, "resident_batches": len(batches),
+                   "mean_reads_per_site": round(float(np.mean(reads)) / S, 2),
+                   "parallelism": f"region-sharded x{world}, no collectives"},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "ss_score_main",
+            "achieved": round(achieved, 2) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "avg_kernel_ms": round(avg_kernel_ms, 4) if avg_kernel_ms else None,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        pre = score[0][: args.cpu_sample].cpu().numpy() if S >= args.cpu_sample else None
+        result["cpu_baseline"] = cpu_baseline(args.lt, args.ln, min(args.cpu_sample, S), args.seed, pre)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,468 @@
+/*
+ * oracle/ss_oracle.c -- CPU restatement of SomaticSniper's per-site scorer.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The
+ * product (somatic-sniper_amd/, libsniper_amd.so) never links or calls it.
+ *
+ * Pinned against the real reference: oracle/ref.mk compiles /root/reference into
+ * oracle/_ref/ref_harness, whose per-site dumps are committed as golden vectors
+ * under tests/golden/ (generator: tests/golden/make_golden.py) and checked
+ * bit-exactly by tests/test_oracle_golden.py.
+ *
+ * Arithmetic is restated with the reference's exact C types (float accumulators,
+ * double increments, x87 long double table terms) so every integer output --
+ * glf1_t.lk, consensus words, posterior sums -- is identical.  Build with
+ * -ffp-contract=off and without -ffast-math.
+ *
+ * Each function cites the reference code it restates (paths relative to
+ * /root/reference/src/lib/sniper unless noted).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "sniper_amd.h"   /* packed read layout, ss_params_t, ss_glf_t, ss_call_t */
+
+#define ORC_PHRED 4.343   /* PHRED_CONST, somatic_sniper.h:12 */
+
+typedef struct orc_model {
+    ss_params_t prm;
+    double  fk[256];
+    double *coef;          /* [64<<16], index q<<16 | n<<8 | k */
+    double *lhet;          /* [256*256], index n1<<8 | n2 */
+    float   q_r;
+    int     q_r_int;       /* (int)(q_r + .5), sniper_maqcns.c:279 */
+    int     qadd[1024];
+    int     prior[16][10];
+    int     jprior[16][10][10];
+    uint32_t *scratch;     /* key buffer (the reference's bm->aux->info) */
+    int      scratch_cap;
+} orc_model_t;
+
+/* ---- nt16 mapping (samtools-0.1.6/bam_import.c:23-40, rev table :61) ------ */
+static unsigned char orc_nt16[256];
+static void orc_nt16_init(void)
+{
+    static const char rev[] = "=ACMGRSVTWYHKDBN";
+    int i;
+    for (i = 0; i < 256; ++i) orc_nt16[i] = 15;
+    for (i = 0; i < 16; ++i) {
+        orc_nt16[(unsigned char)rev[i]] = (unsigned char)i;
+        if (rev[i] >= 'A' && rev[i] <= 'Z') orc_nt16[(unsigned char)(rev[i] + 32)] = (unsigned char)i;
+    }
+    /* colour-space digits map to bases in samtools 0.1.6 */
+    orc_nt16['0'] = 1; orc_nt16['1'] = 2; orc_nt16['2'] = 4; orc_nt16['3'] = 8;
+    orc_nt16['N'] = orc_nt16['n'] = 15;
+}
+static const int orc_nt4_of_nt16[16] = {4, 0, 1, 4, 2, 4, 4, 4, 3, 4, 4, 4, 4, 4, 4, 4}; /* sniper_maqcns.c:19 */
+
+/* logPhred / expPhred, somatic_sniper.h:13-14 */
+static int orc_log_phred(double x)
+{
+    return (int)(x < 1 ? (0.5 - ORC_PHRED * log(x)) : (-0.5 - ORC_PHRED * log(x)));
+}
+static double orc_exp_phred(int x) { return (double)exp((double)(-(x)) / ORC_PHRED); }
+
+/* glfBase / isHom / isHet, somatic_sniper.c:24-26 */
+static const int orc_gl_base[10] = {1, 3, 5, 9, 2, 6, 10, 4, 12, 8};
+static int orc_is_hom(int b) { return b == 1 || b == 2 || b == 4 || b == 8; }
+static int orc_is_het(int b) { return b == 3 || b == 5 || b == 6 || b == 9 || b == 10 || b == 12; }
+
+/* ---- tables: sniper_cal_coef (sniper_maqcns.c:59-100) --------------------- */
+static void orc_build_coef(orc_model_t *m)
+{
+    long double tail[257], beta[256], acc[256], term[256], fk_half[256];
+    double *lbin = (double *)calloc(256 * 256, sizeof(double));
+    int n, k, q;
+    m->coef = (double *)calloc(256 * 256 * 64, sizeof(double));
+    m->fk[0] = 1.0;
+    fk_half[0] = 1.0;
+    for (n = 1; n < 256; ++n) {
+        m->fk[n] = pow(m->prm.theta, n) * (1.0 - m->prm.eta) + m->prm.eta;
+        fk_half[n] = m->fk[n >> 1];
+    }
+    for (n = 1; n < 256; ++n)
+        for (k = 1; k <= n; ++k)
+            lbin[n << 8 | k] = lgamma(n + 1) - lgamma(k + 1) - lgamma(n - k + 1);
+    for (q = 1; q < 64; ++q) {
+        double e = pow(10.0, -q / 10.0);
+        double le = log(e), le1 = log(1.0 - e);
+        for (n = 1; n < 256; ++n) {
+            double *row = m->coef + (q << 16 | n << 8);
+            tail[n + 1] = 0.0;
+            for (k = n; k >= 0; --k) {
+                tail[k] = tail[k + 1] + expl(lbin[n << 8 | k] + k * le + (n - k) * le1);
+                beta[k] = tail[k + 1] / tail[k];
+                if (beta[k] > 0.99) beta[k] = 0.99;
+            }
+            for (k = 0; k < n; ++k) acc[k] = -4.343 * fk_half[k] * logl(beta[k] / e);
+            for (k = 1; k < n; ++k) acc[k] += acc[k - 1];
+            for (k = 0; k <= n; ++k) {
+                term[k] = -4.343 * logl(1.0 - expl(fk_half[k] * logl(beta[k])));
+                row[k] = (k ? acc[k - 1] : 0) + term[k];
+            }
+        }
+    }
+    free(lbin);
+}
+
+/* ---- tables: sniper_cal_het (sniper_maqcns.c:27-56) ----------------------- */
+static void orc_build_het(orc_model_t *m)
+{
+    double harm = 0.0, poly;
+    int k, a, b;
+    m->lhet = (double *)calloc(256 * 256, sizeof(double));
+    for (k = 1; k <= m->prm.n_hap - 1; ++k) harm += 1.0 / k;
+    for (a = 0; a < 256; ++a) {
+        for (b = 0; b < 256; ++b) {
+            long double s = 0.0;
+            double lc = lgamma(a + b + 1) - lgamma(a + 1) - lgamma(b + 1);
+            for (k = 1; k <= m->prm.n_hap - 1; ++k) {
+                double pk = 1.0 / k / harm;
+                double l1 = log((double)k / m->prm.n_hap);
+                double l2 = log(1.0 - (double)k / m->prm.n_hap);
+                s += pk * 0.5 * (expl(l1 * b) * expl(l2 * a) + expl(l1 * a) * expl(l2 * b));
+            }
+            m->lhet[a << 8 | b] = lc + logl(s);
+        }
+    }
+    poly = m->prm.het_rate * harm;
+    m->q_r = -4.343 * log(2.0 * poly / (1.0 - poly));
+    m->q_r_int = (int)(m->q_r + .5);
+}
+
+/* ---- qAddTableInit / makeSoloPrior / make_joint_prior ----------------------
+ * somatic_sniper.c:101-107, :29-45, :47-77.  qadd[1000..1023] stay 0 (static
+ * storage never written by the reference). */
+static void orc_build_phred_tables(orc_model_t *m)
+{
+    const double THETA = 0.001; /* somatic_sniper.c:14 */
+    int i, j, r;
+    memset(m->qadd, 0, sizeof(m->qadd));
+    for (i = 0; i < 1000; ++i) m->qadd[i] = orc_log_phred(1 + orc_exp_phred(i - 512));
+    memset(m->prior, 0, sizeof(m->prior));
+    memset(m->jprior, 0, sizeof(m->jprior));
+    for (r = 0; r < 16; ++r) {
+        for (i = 0; i < 10; ++i) {
+            int b = orc_gl_base[i], g;
+            if (!(b & ~r)) g = 0;
+            else if (b & r) g = orc_log_phred(THETA);
+            else if (orc_is_hom(b)) g = orc_log_phred(0.5 * THETA);
+            else g = orc_log_phred(THETA * THETA);
+            if (m->prm.use_priors) m->prior[r][i] = g;
+            if (m->prm.use_joint_priors) {
+                double sr = m->prm.somatic_rate;
+                for (j = 0; j < 10; ++j) {
+                    int c = orc_gl_base[j];
+                    /* isHet[]/isHom[] are indexed by the genotype INDEX j here,
+                     * not by its base code (somatic_sniper.c:66-70): for j = 0
+                     * (AA) and j = 7 (GG) neither holds, so they fall through to
+                     * the rate^2 branches. */
+                    if (b == c) m->jprior[r][i][j] = g;
+                    else if ((b & c) && (orc_is_het(j) || orc_is_hom(j)))
+                        m->jprior[r][i][j] = g + orc_log_phred(sr);
+                    else m->jprior[r][i][j] = g + orc_log_phred(sr * sr);
+                }
+            }
+        }
+    }
+}
+
+orc_model_t *orc_model_create(const ss_params_t *p)
+{
+    orc_model_t *m = (orc_model_t *)calloc(1, sizeof(orc_model_t));
+    orc_nt16_init();
+    m->prm = *p;
+    orc_build_coef(m);
+    orc_build_het(m);
+    orc_build_phred_tables(m);
+    return m;
+}
+
+void orc_model_destroy(orc_model_t *m)
+{
+    if (!m) return;
+    free(m->coef); free(m->lhet); free(m->scratch); free(m);
+}
+
+const double *orc_model_fk(const orc_model_t *m) { return m->fk; }
+const double *orc_model_coef(const orc_model_t *m) { return m->coef; }
+const double *orc_model_lhet(const orc_model_t *m) { return m->lhet; }
+float orc_model_q_r(const orc_model_t *m) { return m->q_r; }
+const int *orc_model_qadd(const orc_model_t *m) { return m->qadd; }
+const int *orc_model_prior(const orc_model_t *m) { return &m->prior[0][0]; }
+const int *orc_model_jprior(const orc_model_t *m) { return &m->jprior[0][0][0]; }
+int orc_nt16_of(int ch) { orc_nt16_init(); return orc_nt16[ch & 0xff]; }
+
+static int orc_cmp_u32(const void *a, const void *b)
+{
+    uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* ---- sniper_maqcns_glfgen (sniper_maqcns.c:127-248) ------------------------
+ * reads: packed non-deleted reads; n == 0 gives depth 0 (the caller treats the
+ * site as skipped, somatic_sniper.c:127). */
+void orc_glfgen(orc_model_t *m, const uint32_t *reads, int n, int ref_nt16, ss_glf_t *g)
+{
+    float esum[4] = {0, 0, 0, 0}, fsum[4] = {0, 0, 0, 0};
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    int w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float p[16], min_p = 1e30;
+    uint64_t rms = 0;
+    int i, j, k, tot;
+    uint8_t rms_q;
+
+    memset(g, 0, sizeof(*g));
+    g->ref_base = (uint8_t)ref_nt16;
+    if (n == 0) return;
+    if (m->scratch_cap < n) {
+        m->scratch_cap = n * 2;
+        m->scratch = (uint32_t *)realloc(m->scratch, 4 * (size_t)m->scratch_cap);
+    }
+    /* sort keys, :144-157 */
+    for (i = 0; i < n; ++i) {
+        uint32_t r = reads[i], bq = SS_READ_BASEQ(r), mq = SS_READ_MAPQ(r), b = SS_READ_NT16(r);
+        uint32_t key = SS_READ_STRAND(r) << 18 | bq << 8 | mq, nt4;
+        key |= (mq < bq ? mq : bq) << 24;
+        nt4 = (uint32_t)orc_nt4_of_nt16[b ? b : (uint32_t)ref_nt16];
+        if (nt4 < 4) key |= 1u << 21 | nt4 << 16;
+        m->scratch[i] = key;
+    }
+    qsort(m->scratch, (size_t)n, 4, orc_cmp_u32);
+    /* ordered fold, descending key, :160-176 */
+    for (j = n - 1; j >= 0; --j) {
+        uint32_t key = m->scratch[j];
+        int t;
+        if (key >> 24 < 4 && (key >> 8 & 0x3f) != 0) key = 4u << 24 | (key & 0xffffff);
+        k = key >> 16 & 7;
+        if (key >> 24 > 0) {
+            esum[k & 3] += m->fk[w[k]] * (key >> 24);
+            fsum[k & 3] += m->fk[w[k]];
+            if (w[k] < 0xff) ++w[k];
+            ++cnt[k & 3];
+        }
+        t = (int)(key & 0x7f) < m->prm.cap_mapQ ? (int)(key & 0x7f) : m->prm.cap_mapQ;
+        rms += (uint64_t)(t * t);
+    }
+    rms_q = (uint8_t)(sqrt((double)rms / n) + .499);
+    /* rescale counts, :178-182 */
+    for (j = tot = 0; j < 4; ++j) tot += cnt[j];
+    if (tot > 255) {
+        for (j = 0; j < 4; ++j) cnt[j] = (int)(254.0 * cnt[j] / tot + 0.5);
+        for (j = tot = 0; j < 4; ++j) tot += cnt[j];
+    }
+    /* genotype likelihoods, :184-214 */
+    for (j = 0; j < 4; ++j) {
+        float e1 = 0.0f, f1 = 0.0f;
+        int c2 = 0, be;
+        for (k = 0; k < 4; ++k) {
+            if (k == j) continue;
+            e1 += esum[k]; c2 += cnt[k]; f1 += fsum[k];
+        }
+        if (c2) {
+            be = (int)(e1 / f1 + 0.5);
+            be = be < 4 ? 4 : (be > 63 ? 63 : be);
+            p[j << 2 | j] = e1 + m->coef[be << 16 | tot << 8 | c2];
+        } else {
+            p[j << 2 | j] = 0.0;
+        }
+        for (k = j + 1; k < 4; ++k) {
+            float e2 = 0.0f, f2 = 0.0f;
+            int c3 = 0;
+            for (i = 0; i < 4; ++i) {
+                if (i == j || i == k) continue;
+                e2 += esum[i]; c3 += cnt[i]; f2 += fsum[i];
+            }
+            if (c3) {
+                be = (int)(e2 / f2 + 0.5);
+                be = be < 4 ? 4 : (be > 63 ? 63 : be);
+                p[j << 2 | k] = p[k << 2 | j] =
+                    -4.343 * m->lhet[cnt[j] << 8 | cnt[k]] + e2 + m->coef[be << 16 | tot << 8 | c3];
+            } else {
+                p[j << 2 | k] = p[k << 2 | j] = -4.343 * m->lhet[cnt[j] << 8 | cnt[k]];
+            }
+        }
+        for (k = 0; k < 4; ++k)
+            if (p[j << 2 | k] < 0.0) p[j << 2 | k] = 0.0;
+    }
+    /* adjust the hom genotype of the best-supported base, :216-233 */
+    {
+        float hi1 = -1.0, hi2 = -1.0, lo1 = 1e30, lo2 = 1e30;
+        int hik = -1, lok = -1;
+        for (k = 0; k < 4; ++k) {
+            if (esum[k] > hi1) { hi2 = hi1; hi1 = esum[k]; hik = k; }
+            else if (esum[k] > hi2) hi2 = esum[k];
+        }
+        for (k = 0; k < 4; ++k) {
+            if (p[k << 2 | k] < lo1) { lo2 = lo1; lo1 = p[k << 2 | k]; lok = k; }
+            else if (p[k << 2 | k] < lo2) lo2 = p[k << 2 | k];
+        }
+        if (hi1 > hi2 && (lok != hik || lo1 + 1.0 > lo2))
+            p[hik << 2 | hik] = lo1 > 1.0 ? lo1 - 1.0 : 0.0;
+    }
+    /* quantise, :235-244 */
+    g->max_mapQ = rms_q;
+    g->depth = n > 16777215 ? 16777215u : (uint32_t)n;
+    for (j = 0; j < 4; ++j)
+        for (k = j; k < 4; ++k)
+            if (p[j << 2 | k] < min_p) min_p = p[j << 2 | k];
+    g->min_lk = min_p > 255.0 ? 255 : (int)(min_p + 0.5);
+    for (j = i = 0; j < 4; ++j)
+        for (k = j; k < 4; ++k)
+            g->lk[i++] = p[j << 2 | k] - min_p > 255.0 ? 255 : (int)(p[j << 2 | k] - min_p + 0.5);
+}
+
+/* ---- sniper_glf2cns (sniper_maqcns.c:250-273) ----------------------------- */
+uint32_t orc_glf2cns(const ss_glf_t *g, int q_r)
+{
+    int s[10], i, b1 = 10000, b2 = 10000, b3 = 10000, g1 = -1, g2 = -1;
+    static const int gi[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+    static const int gj[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+    uint32_t x;
+    /* upper-triangle scan order i<<2|j equals lk[] order */
+    for (i = 0; i < 10; ++i) s[i] = g->lk[i] + (gi[i] == gj[i] ? 0 : q_r);
+    for (i = 0; i < 10; ++i) {
+        if (s[i] < b1) { b3 = b2; b2 = b1; b1 = s[i]; g2 = g1; g1 = i; }
+        else if (s[i] < b2) { b3 = b2; b2 = s[i]; g2 = i; }
+        else if (s[i] < b3) b3 = s[i];
+    }
+    x = g1 >= 0 ? (1u << gi[g1] | 1u << gj[g1]) << 28 : 0xfu << 28;
+    x |= g2 >= 0 ? (1u << gi[g2] | 1u << gj[g2]) << 24 : 0xfu << 24;
+    x |= (uint32_t)g->max_mapQ << 16;
+    x |= b2 < 10000 ? (uint32_t)(b2 - b1 < 256 ? b2 - b1 : 255) << 8 : 0xffu << 8;
+    x |= b2 < 10000 && b3 < 10000 ? (uint32_t)(b3 - b2 < 256 ? b3 - b2 : 255) : 0xffu;
+    return x;
+}
+
+/* qAdd macro, somatic_sniper.c:18: qAdd(x,y) = x + T[512+y-x]; out-of-range
+ * indices (reference UB) are clamped and counted. */
+static int orc_qadd(const orc_model_t *m, int x, int y, int *clamped)
+{
+    int idx = 512 + y - x;
+    if (idx < 0) { idx = 0; ++*clamped; }
+    else if (idx > 1023) { idx = 1023; ++*clamped; }
+    return x + m->qadd[idx];
+}
+
+/* calculatePosteriors, somatic_sniper.c:79-99 */
+static void orc_posteriors(const orc_model_t *m, const ss_glf_t *g, int *lk, int *clamped)
+{
+    int sum = 255, j;
+    for (j = 0; j < 10; ++j) {
+        int x = g->lk[j] + m->prior[g->ref_base][j];
+        sum = orc_qadd(m, x, sum, clamped);
+        lk[j] = x;
+    }
+    for (j = 0; j < 10; ++j) {
+        lk[j] -= sum;
+        if (lk[j] > 255) lk[j] = 255;
+    }
+}
+
+/* ---- glf_somatic body (somatic_sniper.c:109-273) ---------------------------
+ * Returns the callback's return value; fills *call (emit decision in
+ * call->flags bit 7) and both glf records. */
+#define ORC_EMIT 0x80
+int orc_site(orc_model_t *m, int ref_char, const uint32_t *rt, int nt, const uint32_t *rn,
+             int nn, ss_glf_t *gt, ss_glf_t *gn, ss_call_t *call)
+{
+    const int rb = ref_char & 0xff, rb4 = orc_nt16[rb];
+    int qps = 255, clamped = 0;
+    uint32_t ct, cn;
+    int t1, t2, ts1, ts2, n1, n2, ns1, ns2, tq = 0, nq = 0, jt = 0, jn = 0, jcq = 255;
+    int lkt[10], lkn[10], tg, ng;
+
+    memset(call, 0, sizeof(*call));
+    orc_glfgen(m, rt, nt, rb4, gt);
+    orc_glfgen(m, rn, nn, rb4, gn);
+    if (!(rb != 'N' && gt->depth > 0 && gn->depth > 0)) return -1;
+    ct = orc_glf2cns(gt, m->q_r_int);
+    cn = orc_glf2cns(gn, m->q_r_int);
+    t1 = ct >> 28; t2 = ct >> 24 & 0xf; ts1 = ct >> 8 & 0xff; ts2 = ct & 0xff;
+    n1 = cn >> 28; n2 = cn >> 24 & 0xf; ns1 = cn >> 8 & 0xff; ns2 = cn & 0xff;
+    call->cns_tumor = ct;
+    call->cns_normal = cn;
+    call->ref_base4 = (uint8_t)rb4;
+    if (!(rb4 != 15 && t1 != 15 && n1 != 15 && t1 != n1)) return 255;
+
+    tq = t2 == rb4 ? ts1 : ts1 + ts2;
+    if (tq > 255) tq = 255;
+    if (n1 != 15 && n1 != rb4) {
+        nq = n2 == rb4 ? ns1 : ns1 + ns2;
+        if (nq > 255) nq = 255;
+    }
+    orc_posteriors(m, gt, lkt, &clamped);
+    orc_posteriors(m, gn, lkn, &clamped);
+    if (m->prm.use_joint_priors) {
+        int jl[10][10], marg = 255, bi = -1, bj = -1, best = 1000, i, j;
+        for (i = 0; i < 10; ++i)
+            for (j = 0; j < 10; ++j) {
+                jl[i][j] = (int)gn->lk[i] + (int)gt->lk[j] + m->jprior[rb4][i][j];
+                if (jl[i][j] > 255) jl[i][j] = 255;
+                if (jl[i][j] < best) { best = jl[i][j]; bi = i; bj = j; }
+                marg = orc_qadd(m, marg, jl[i][j], &clamped);
+            }
+        for (j = 0; j < 10; ++j) {
+            int l = jl[j][j] - marg;
+            qps = orc_qadd(m, qps, l, &clamped);
+            /* reference tests a stale loop index (i == 10) here, so only the
+             * tumor condition is live: somatic_sniper.c:196 */
+            if (j != bj) jcq = orc_qadd(m, jcq, l, &clamped);
+        }
+        if (jcq > 255) jcq = 255;
+        jn = orc_gl_base[bi];
+        jt = orc_gl_base[bj];
+    } else {
+        int j;
+        for (j = 0; j < 10; ++j) qps = orc_qadd(m, qps, lkt[j] + lkn[j], &clamped);
+    }
+    tg = jt ? jt : t1;
+    ng = jn ? jn : n1;
+    call->somatic_score = qps;
+    call->snp_q_tumor = (uint8_t)tq;
+    call->snp_q_normal = (uint8_t)nq;
+    call->joint_gt_tumor = (uint8_t)jt;
+    call->joint_gt_normal = (uint8_t)jn;
+    call->joint_cq = (int16_t)jcq;
+    /* allele_util.h:26-27 / allele_util.c:19-28 */
+#define ORC_PSUB(a, b) ((b) != (a) && ((a) & (b)) == (a))
+    call->status_tumor = tg == ng ? SS_GERMLINE
+                       : ORC_PSUB(tg, ng) ? SS_LOH : (qps > 0 ? SS_SOMATIC : SS_UNKNOWN);
+    call->status_normal = n1 == rb4 ? SS_WILDTYPE : SS_GERMLINE;
+    if (clamped) call->flags |= SS_CALL_QADD_CLAMPED;
+    if (m->prm.min_somatic_qual <= qps &&
+        (m->prm.include_loh || !ORC_PSUB(tg, ng)) &&
+        (m->prm.include_gor || !(!ORC_PSUB(rb4, ng) && (tg & ~ng) == rb4)))
+        call->flags |= ORC_EMIT;
+#undef ORC_PSUB
+    return qps;
+}
+
+/* Score a host CSR batch.  glf may be NULL; calls receives every EMITTED site in
+ * order (up to cap); returns the number of emitted sites. */
+long orc_score_batch(orc_model_t *m, uint64_t n_sites, const uint8_t *ref,
+                     const uint32_t *off_t, const uint32_t *off_n,
+                     const uint32_t *reads_t, const uint32_t *reads_n,
+                     int32_t *score, ss_glf_t *glf, ss_call_t *calls, long cap)
+{
+    uint64_t i;
+    long ne = 0;
+    for (i = 0; i < n_sites; ++i) {
+        ss_glf_t g2[2];
+        ss_call_t c;
+        int r = orc_site(m, ref[i], reads_t + off_t[i], (int)(off_t[i + 1] - off_t[i]),
+                         reads_n + off_n[i], (int)(off_n[i + 1] - off_n[i]), &g2[0], &g2[1], &c);
+        score[i] = r;
+        if (glf) { glf[2 * i] = g2[0]; glf[2 * i + 1] = g2[1]; }
+        if (r >= 0 && (c.flags & ORC_EMIT)) {
+            c.flags &= (uint8_t)~ORC_EMIT;
+            c.site = (uint32_t)i;
+            if (calls && ne < cap) calls[ne] = c;
+            ++ne;
+        }
+    }
+    return ne;
+}

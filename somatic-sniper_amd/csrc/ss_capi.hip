@@ -1,0 +1,448 @@
+/*
+ * ss_capi.hip -- the C ABI (include/sniper_amd.h): contexts, table upload,
+ * batch launches, host-buffer convenience path, device synthetic generator.
+ *
+ * Memory layout in HBM per context (DESIGN.md "Data layout"):
+ *   model   coef 32 MiB + lhet 512 KiB + fk 2 KiB + qadd/prior/jprior/nt16 12 KiB
+ *           (read-only, stays resident in L2/MALL after the first batches)
+ *   lists   deep/giant site lists + counters, giant scratch 64 MiB
+ *   host-path staging buffers, grown on demand
+ */
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "sniper_amd.h"
+#include "ss_host.h"
+#include "ss_kernels.h"
+#include "ss_synth.h"
+
+struct ss_ctx {
+    int device;
+    int n_cu;
+    ss_host_model_t hm;
+    /* model on the device */
+    double *d_fk, *d_coef, *d_lhet;
+    int32_t *d_qadd, *d_prior, *d_jprior;
+    uint8_t *d_nt16;
+    /* work lists */
+    uint32_t *d_counters;     /* [0] deep, [1] giant, [2] err, [3] scratch n_calls, [4] clamped */
+    uint32_t *d_deep_list;
+    uint32_t deep_cap;
+    uint32_t *d_giant_list;
+    uint32_t giant_cap;
+    uint32_t *d_giant_scratch;
+    uint32_t giant_keys;
+    /* timing: a pool of event pairs, one pair per launch while enabled */
+    int timing;
+    std::vector<hipEvent_t> *ev;
+    int n_logged;
+    hipStream_t last_stream;
+    /* host path */
+    hipStream_t hstream;
+    void *h_stage;  size_t h_stage_sz;     /* pinned */
+    void *d_stage;  size_t d_stage_sz;
+    /* synth */
+    uint32_t *d_cdf;                        /* [2][SS_SYNTH_MAXCDF] */
+    void *d_scan_tmp; size_t scan_tmp_sz;
+    uint32_t *d_depth_tmp; size_t depth_tmp_n;
+};
+
+#define HIPCHK(x)                                   \
+    do {                                            \
+        if ((x) != hipSuccess) return SS_E_HIP;     \
+    } while (0)
+
+extern "C" int ss_abi_version(void) { return SS_ABI_VERSION; }
+
+extern "C" const char *ss_strerror(int code)
+{
+    switch (code) {
+    case SS_OK: return "ok";
+    case SS_E_INVAL: return "invalid argument or malformed batch";
+    case SS_E_HIP: return "HIP runtime error";
+    case SS_E_NOMEM: return "out of memory";
+    case SS_E_TABLES: return "host model tables differ from the reference (libm mismatch)";
+    case SS_E_CAPACITY: return "capacity exceeded (emitted calls, work lists or pileup depth)";
+    case SS_E_NODEV: return "no usable HIP device";
+    default: return "unknown error";
+    }
+}
+
+static int dev_alloc(void **p, size_t bytes)
+{
+    if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) { *p = nullptr; return SS_E_NOMEM; }
+    return SS_OK;
+}
+
+template <typename T>
+static int upload(T **dst, const T *src, size_t n)
+{
+    int rc = dev_alloc((void **)dst, n * sizeof(T));
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return SS_OK;
+}
+
+extern "C" void ss_ctx_destroy(ss_ctx_t *c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipDeviceSynchronize();
+    void *ptrs[] = {c->d_fk, c->d_coef, c->d_lhet, c->d_qadd, c->d_prior, c->d_jprior, c->d_nt16,
+                    c->d_counters, c->d_deep_list, c->d_giant_list, c->d_giant_scratch, c->d_stage,
+                    c->d_cdf, c->d_scan_tmp, c->d_depth_tmp};
+    for (void *p : ptrs)
+        if (p) hipFree(p);
+    if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->ev) {
+        for (hipEvent_t e : *c->ev) hipEventDestroy(e);
+        delete c->ev;
+    }
+    if (c->hstream) hipStreamDestroy(c->hstream);
+    ss_host_model_free(&c->hm);
+    free(c);
+}
+
+extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
+{
+    int ndev = 0, rc;
+    if (!p || !out) return SS_E_INVAL;
+    *out = nullptr;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SS_E_NODEV;
+    if (device < 0 || device >= ndev) return SS_E_NODEV;
+    ss_ctx_t *c = (ss_ctx_t *)calloc(1, sizeof(ss_ctx_t));
+    if (!c) return SS_E_NOMEM;
+    c->device = device;
+    c->ev = new std::vector<hipEvent_t>();
+    if ((rc = ss_host_model_build(p, &c->hm)) != SS_OK) { delete c->ev; free(c); return rc; }
+    if (hipSetDevice(device) != hipSuccess) { ss_ctx_destroy(c); return SS_E_HIP; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) { ss_ctx_destroy(c); return SS_E_HIP; }
+    c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+#define TRY(x) do { if ((rc = (x)) != SS_OK) { ss_ctx_destroy(c); return rc; } } while (0)
+    TRY(upload(&c->d_fk, c->hm.fk, 256));
+    TRY(upload(&c->d_coef, c->hm.coef, (size_t)64 << 16));
+    TRY(upload(&c->d_lhet, c->hm.lhet, 65536));
+    TRY(upload(&c->d_qadd, c->hm.qadd, 1024));
+    TRY(upload(&c->d_prior, c->hm.prior, 160));
+    TRY(upload(&c->d_jprior, c->hm.jprior, 1600));
+    TRY(upload(&c->d_nt16, (const uint8_t *)ss_nt16_table, 256));
+    TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t)));
+    c->giant_cap = 1u << 16;
+    TRY(dev_alloc((void **)&c->d_giant_list, c->giant_cap * sizeof(uint32_t)));
+    c->giant_keys = 1u << 20;
+    TRY(dev_alloc((void **)&c->d_giant_scratch,
+                  (size_t)SS_GIANT_BLOCKS * 2 * c->giant_keys * sizeof(uint32_t)));
+    TRY(dev_alloc((void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t)));
+#undef TRY
+    if (hipMemset(c->d_counters, 0, 16 * sizeof(uint32_t)) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess) {
+        ss_ctx_destroy(c);
+        return SS_E_HIP;
+    }
+    *out = c;
+    return SS_OK;
+}
+
+extern "C" int ss_table_hashes(const ss_ctx_t *c, uint64_t *fk, uint64_t *coef, uint64_t *lhet,
+                               float *q_r)
+{
+    if (!c) return SS_E_INVAL;
+    if (fk) *fk = c->hm.h_fk;
+    if (coef) *coef = c->hm.h_coef;
+    if (lhet) *lhet = c->hm.h_lhet;
+    if (q_r) *q_r = c->hm.q_r;
+    return SS_OK;
+}
+
+extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double *lhet,
+                             int *qadd, int *prior, int *jprior)
+{
+    if (!c) return SS_E_INVAL;
+    if (fk) memcpy(fk, c->hm.fk, sizeof(c->hm.fk));
+    if (coef) memcpy(coef, c->hm.coef, ((size_t)64 << 16) * sizeof(double));
+    if (lhet) memcpy(lhet, c->hm.lhet, 65536 * sizeof(double));
+    if (qadd) memcpy(qadd, c->hm.qadd, sizeof(c->hm.qadd));
+    if (prior) memcpy(prior, c->hm.prior, sizeof(c->hm.prior));
+    if (jprior) memcpy(jprior, c->hm.jprior, sizeof(c->hm.jprior));
+    return SS_OK;
+}
+
+static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites)
+{
+    if (n_sites <= c->deep_cap) return SS_OK;
+    uint64_t cap = std::max<uint64_t>(n_sites, 1u << 16);
+    if (cap > 0xffffffffull) return SS_E_INVAL;
+    if (c->d_deep_list) {
+        hipDeviceSynchronize();
+        hipFree(c->d_deep_list);
+        c->d_deep_list = nullptr;
+    }
+    c->deep_cap = 0;
+    if (dev_alloc((void **)&c->d_deep_list, cap * sizeof(uint32_t))) return SS_E_NOMEM;
+    c->deep_cap = (uint32_t)cap;
+    return SS_OK;
+}
+
+extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_out_t *o, void *stream)
+{
+    if (!c || !b || !o || !o->score) return SS_E_INVAL;
+    if (b->n_sites == 0) return SS_OK;
+    if (b->n_sites >= 0xffffffffull) return SS_E_INVAL;
+    if (!b->ref || !b->off_tumor || !b->off_normal || !b->reads_tumor || !b->reads_normal)
+        return SS_E_INVAL;
+    if (o->calls && !o->n_calls) return SS_E_INVAL;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = ensure_deep_cap(c, b->n_sites);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    /* counters: deep, giant, (err is sticky), scratch n_calls, scratch clamped */
+    HIPCHK(hipMemsetAsync(c->d_counters, 0, 2 * sizeof(uint32_t), s));
+    if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
+    ss_score_args a;
+    memset(&a, 0, sizeof(a));
+    a.n_sites = b->n_sites;
+    a.ref = b->ref;
+    a.off_t = b->off_tumor;
+    a.off_n = b->off_normal;
+    a.reads_t = b->reads_tumor;
+    a.reads_n = b->reads_normal;
+    a.score = o->score;
+    a.calls = o->calls;
+    a.calls_cap = o->calls ? o->calls_cap : 0;
+    a.n_calls = o->n_calls ? o->n_calls : c->d_counters + 3;
+    a.glf = o->glf;
+    a.n_clamped = o->n_qadd_clamped;
+    a.deep_list = c->d_deep_list;
+    a.deep_count = c->d_counters + 0;
+    a.deep_cap = c->deep_cap;
+    a.giant_list = c->d_giant_list;
+    a.giant_count = c->d_counters + 1;
+    a.giant_cap = c->giant_cap;
+    a.giant_scratch = c->d_giant_scratch;
+    a.giant_keys = c->giant_keys;
+    a.err = c->d_counters + 2;
+    a.m.fk = c->d_fk;
+    a.m.coef = c->d_coef;
+    a.m.lhet = c->d_lhet;
+    a.m.qadd = c->d_qadd;
+    a.m.prior = c->d_prior;
+    a.m.jprior = c->d_jprior;
+    a.m.nt16 = c->d_nt16;
+    a.m.q_r_int = c->hm.q_r_int;
+    a.m.cap_mapQ = c->hm.prm.cap_mapQ;
+    a.m.min_somatic_qual = c->hm.prm.min_somatic_qual;
+    a.m.use_joint = c->hm.prm.use_joint_priors;
+    a.m.include_loh = c->hm.prm.include_loh;
+    a.m.include_gor = c->hm.prm.include_gor;
+    const uint64_t groups = (b->n_sites + 7) / 8;
+    uint64_t blocks = (groups + 3) / 4;
+    const uint64_t max_blocks = (uint64_t)c->n_cu * 32;
+    if (blocks > max_blocks) blocks = max_blocks;
+    const int deep_grid = c->n_cu * 4;
+    c->last_stream = s;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing && c->n_logged < 4096) {
+        while ((int)c->ev->size() < 2 * (c->n_logged + 1)) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return SS_E_HIP;
+            c->ev->push_back(e);
+        }
+        e0 = (*c->ev)[2 * c->n_logged];
+        e1 = (*c->ev)[2 * c->n_logged + 1];
+        ++c->n_logged;
+    }
+    int e = ss_launch_score(a, (int)blocks, deep_grid, s, e0, e1);
+    return e == 0 ? SS_OK : SS_E_HIP;
+}
+
+extern "C" int ss_set_kernel_timing(ss_ctx_t *c, int enable)
+{
+    if (!c) return SS_E_INVAL;
+    c->timing = enable ? 1 : 0;
+    if (enable) c->n_logged = 0;
+    return SS_OK;
+}
+
+static double pair_ms(ss_ctx_t *c, int i)
+{
+    float ms = -1.0f;
+    if (hipEventSynchronize((*c->ev)[2 * i + 1]) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, (*c->ev)[2 * i], (*c->ev)[2 * i + 1]) != hipSuccess) return -1.0;
+    return ms;
+}
+
+extern "C" double ss_last_kernel_ms(ss_ctx_t *c)
+{
+    if (!c || c->n_logged == 0) return -1.0;
+    hipSetDevice(c->device);
+    return pair_ms(c, c->n_logged - 1);
+}
+
+extern "C" int ss_kernel_time_log(ss_ctx_t *c, double *ms, int cap)
+{
+    int i, n;
+    if (!c || (!ms && cap)) return SS_E_INVAL;
+    hipSetDevice(c->device);
+    n = c->n_logged < cap ? c->n_logged : cap;
+    for (i = 0; i < n; ++i) ms[i] = pair_ms(c, i);
+    return n;
+}
+
+extern "C" int ss_ctx_check(ss_ctx_t *c)
+{
+    uint32_t err = 0;
+    if (!c) return SS_E_INVAL;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(&err, c->d_counters + 2, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) {
+        HIPCHK(hipMemset(c->d_counters + 2, 0, sizeof(uint32_t)));
+        return SS_E_CAPACITY;
+    }
+    return SS_OK;
+}
+
+/* ---------------------------------------------------------- host path ---- */
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int ensure_stage(ss_ctx_t *c, size_t bytes)
+{
+    if (bytes <= c->h_stage_sz && bytes <= c->d_stage_sz) return SS_OK;
+    size_t sz = std::max(bytes, (size_t)1 << 20);
+    sz += sz / 4;
+    if (c->h_stage) { hipHostFree(c->h_stage); c->h_stage = nullptr; c->h_stage_sz = 0; }
+    if (c->d_stage) { hipFree(c->d_stage); c->d_stage = nullptr; c->d_stage_sz = 0; }
+    if (hipHostMalloc(&c->h_stage, sz, hipHostMallocDefault) != hipSuccess) return SS_E_NOMEM;
+    c->h_stage_sz = sz;
+    if (hipMalloc(&c->d_stage, sz) != hipSuccess) return SS_E_NOMEM;
+    c->d_stage_sz = sz;
+    return SS_OK;
+}
+
+extern "C" int ss_score_batch_host(ss_ctx_t *c, const ss_batch_t *b, const ss_out_t *o)
+{
+    if (!c || !b || !o || !o->score) return SS_E_INVAL;
+    const uint64_t n = b->n_sites;
+    if (n == 0) { if (o->n_calls) *o->n_calls = 0; return SS_OK; }
+    if (n >= 0xffffffffull) return SS_E_INVAL;
+    const uint64_t nt = b->off_tumor[n], nn = b->off_normal[n];
+    if (b->off_tumor[0] != 0 || b->off_normal[0] != 0) return SS_E_INVAL;
+    const uint32_t cap = o->calls ? o->calls_cap : 0;
+    /* one staging area: inputs, then outputs */
+    size_t off = 0;
+    const size_t o_ref = off;   off = align_up(off + n);
+    const size_t o_ot = off;    off = align_up(off + 4 * (n + 1));
+    const size_t o_on = off;    off = align_up(off + 4 * (n + 1));
+    const size_t o_rt = off;    off = align_up(off + 4 * nt);
+    const size_t o_rn = off;    off = align_up(off + 4 * nn);
+    const size_t in_bytes = off;
+    const size_t o_sc = off;    off = align_up(off + 4 * n);
+    const size_t o_cnt = off;   off = align_up(off + 16);
+    const size_t o_calls = off; off = align_up(off + sizeof(ss_call_t) * (size_t)cap);
+    const size_t o_glf = off;   off = align_up(off + (o->glf ? sizeof(ss_glf_t) * 2 * n : 0));
+    const size_t total = off;
+    int rc = ensure_stage(c, total);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    char *h = (char *)c->h_stage, *d = (char *)c->d_stage;
+    memcpy(h + o_ref, b->ref, n);
+    memcpy(h + o_ot, b->off_tumor, 4 * (n + 1));
+    memcpy(h + o_on, b->off_normal, 4 * (n + 1));
+    if (nt) memcpy(h + o_rt, b->reads_tumor, 4 * nt);
+    if (nn) memcpy(h + o_rn, b->reads_normal, 4 * nn);
+    hipStream_t s = c->hstream;
+    HIPCHK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s));
+    ss_batch_t db = {n, (const uint8_t *)(d + o_ref), (const uint32_t *)(d + o_ot),
+                     (const uint32_t *)(d + o_on), (const uint32_t *)(d + o_rt),
+                     (const uint32_t *)(d + o_rn)};
+    ss_out_t dout;
+    memset(&dout, 0, sizeof(dout));
+    dout.score = (int32_t *)(d + o_sc);
+    dout.calls = cap ? (ss_call_t *)(d + o_calls) : nullptr;
+    dout.calls_cap = cap;
+    dout.n_calls = (uint32_t *)(d + o_cnt);
+    dout.n_qadd_clamped = (uint32_t *)(d + o_cnt + 4);
+    dout.glf = o->glf ? (ss_glf_t *)(d + o_glf) : nullptr;
+    HIPCHK(hipMemsetAsync(d + o_cnt, 0, 16, s));
+    rc = ss_score_batch_device(c, &db, &dout, s);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h + o_sc, d + o_sc, total - o_sc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    rc = ss_ctx_check(c);
+    memcpy(o->score, h + o_sc, 4 * n);
+    uint32_t ncalls, nclamp;
+    memcpy(&ncalls, h + o_cnt, 4);
+    memcpy(&nclamp, h + o_cnt + 4, 4);
+    if (o->n_calls) *o->n_calls = ncalls;
+    if (o->n_qadd_clamped) *o->n_qadd_clamped = nclamp;
+    if (cap) {
+        const uint32_t k = std::min(ncalls, cap);
+        ss_call_t *calls = o->calls;
+        memcpy(calls, h + o_calls, sizeof(ss_call_t) * k);
+        std::sort(calls, calls + k, [](const ss_call_t &x, const ss_call_t &y) { return x.site < y.site; });
+    }
+    if (o->glf) memcpy(o->glf, h + o_glf, sizeof(ss_glf_t) * 2 * n);
+    if (rc) return rc;
+    if (o->calls && ncalls > cap) return SS_E_CAPACITY;
+    return SS_OK;
+}
+
+/* ------------------------------------------------------ device synth ---- */
+extern "C" int ss_synth_batch_device(ss_ctx_t *c, const ss_synth_t *s, uint64_t first,
+                                     uint64_t n, uint8_t *ref, uint32_t *off_t, uint32_t *off_n,
+                                     uint32_t *rt, uint32_t *rn, uint64_t *n_rt, uint64_t *n_rn)
+{
+    if (!c || !s || !ref || !off_t || !off_n) return SS_E_INVAL;
+    if (n >= 0xffffffffull) return SS_E_INVAL;
+    std::vector<uint32_t> cdf(2 * SS_SYNTH_MAXCDF);
+    ss_synth_k_t k;
+    int rc = ss_synth_prepare(s, &k, cdf.data(), cdf.data() + SS_SYNTH_MAXCDF);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(c->d_cdf, cdf.data(), cdf.size() * 4, hipMemcpyHostToDevice));
+    k.cdf_tumor = c->d_cdf;
+    k.cdf_normal = c->d_cdf + SS_SYNTH_MAXCDF;
+    hipStream_t st = c->hstream;
+    if (!rt || !rn) {
+        /* pass 1: depths -> exclusive scans -> offsets */
+        if (c->depth_tmp_n < 2 * (n + 1)) {
+            if (c->d_depth_tmp) hipFree(c->d_depth_tmp);
+            c->d_depth_tmp = nullptr;
+            c->depth_tmp_n = 0;
+            if (dev_alloc((void **)&c->d_depth_tmp, 2 * (n + 1) * 4)) return SS_E_NOMEM;
+            c->depth_tmp_n = 2 * (n + 1);
+        }
+        uint32_t *dt = c->d_depth_tmp, *dn = c->d_depth_tmp + (n + 1);
+        HIPCHK(hipMemsetAsync(dt, 0, 2 * (n + 1) * 4, st));
+        if (ss_launch_synth_depth(k, first, n, ref, dt, dn, st)) return SS_E_HIP;
+        size_t need = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, dt, off_t, (int)(n + 1), st));
+        if (need > c->scan_tmp_sz) {
+            if (c->d_scan_tmp) hipFree(c->d_scan_tmp);
+            c->d_scan_tmp = nullptr;
+            c->scan_tmp_sz = 0;
+            if (dev_alloc(&c->d_scan_tmp, need)) return SS_E_NOMEM;
+            c->scan_tmp_sz = need;
+        }
+        size_t sz = c->scan_tmp_sz;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->d_scan_tmp, sz, dt, off_t, (int)(n + 1), st));
+        sz = c->scan_tmp_sz;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->d_scan_tmp, sz, dn, off_n, (int)(n + 1), st));
+        uint32_t tot[2];
+        HIPCHK(hipMemcpyAsync(&tot[0], off_t + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&tot[1], off_n + n, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (n_rt) *n_rt = tot[0];
+        if (n_rn) *n_rn = tot[1];
+        return SS_OK;
+    }
+    if (ss_launch_synth_reads(k, first, n, off_t, off_n, rt, rn, st)) return SS_E_HIP;
+    HIPCHK(hipStreamSynchronize(st));
+    return SS_OK;
+}

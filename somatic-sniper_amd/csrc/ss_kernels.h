@@ -1,0 +1,77 @@
+/* ss_kernels.h -- internal interface between the C ABI (ss_capi.hip) and the
+ * HIP kernels (ss_kernels.hip).  Not installed; plain structs of device
+ * pointers passed to the kernels by value. */
+#ifndef SS_KERNELS_H
+#define SS_KERNELS_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sniper_amd.h"
+#include "ss_synth_core.h"
+
+/* Device copy of the model (built on the host by ss_tables.c). */
+struct ss_dev_model {
+    const double  *fk;       /* [256]            */
+    const double  *coef;     /* [64 << 16]       */
+    const double  *lhet;     /* [65536]          */
+    const int32_t *qadd;     /* [1024]           */
+    const int32_t *prior;    /* [16 * 10]        */
+    const int32_t *jprior;   /* [16 * 10 * 10]   */
+    const uint8_t *nt16;     /* [256]            */
+    int32_t q_r_int;
+    int32_t cap_mapQ;
+    int32_t min_somatic_qual;
+    int32_t use_joint;
+    int32_t include_loh;
+    int32_t include_gor;
+};
+
+/* Per-launch arguments of the scoring kernels. */
+struct ss_score_args {
+    /* batch (device) */
+    uint64_t        n_sites;
+    const uint8_t  *ref;
+    const uint32_t *off_t, *off_n;
+    const uint32_t *reads_t, *reads_n;
+    /* outputs (device) */
+    int32_t   *score;
+    ss_call_t *calls;
+    uint32_t   calls_cap;
+    uint32_t  *n_calls;
+    ss_glf_t  *glf;
+    uint32_t  *n_clamped;
+    /* work lists (device; counters zeroed per launch) */
+    uint32_t  *deep_list;     /* sites with a sample deeper than the main-kernel limit */
+    uint32_t  *deep_count;
+    uint32_t   deep_cap;
+    uint32_t  *giant_list;    /* sites deeper than the LDS limit of the deep kernel */
+    uint32_t  *giant_count;
+    uint32_t   giant_cap;
+    uint32_t  *giant_scratch; /* [giant_blocks][2][giant_keys] */
+    uint32_t   giant_keys;    /* keys per sample per giant block (power of two) */
+    uint32_t  *err;           /* sticky error bits, see SS_KERR_* */
+    ss_dev_model m;
+};
+
+#define SS_KERR_DEEP_OVERFLOW  1u
+#define SS_KERR_GIANT_OVERFLOW 2u
+#define SS_KERR_TOO_DEEP       4u
+
+/* Launch geometry constants shared with the host. */
+#define SS_MAIN_BLOCK      256   /* 4 waves                                    */
+#define SS_MAIN_MAXN       256   /* per-sample depth handled by the main kernel */
+#define SS_DEEP_BLOCK      256
+#define SS_DEEP_MAXN       4096  /* per-sample depth sorted in LDS by the deep kernel */
+#define SS_GIANT_BLOCKS    8
+
+/* Launchers (return hipError_t as int). */
+int ss_launch_score(const ss_score_args &a, int main_grid, int deep_grid, hipStream_t s,
+                    hipEvent_t ev0, hipEvent_t ev1);
+int ss_launch_synth_depth(const ss_synth_k_t &k, uint64_t first, uint64_t n, uint8_t *ref,
+                          uint32_t *dt, uint32_t *dn, hipStream_t s);
+int ss_launch_synth_reads(const ss_synth_k_t &k, uint64_t first, uint64_t n,
+                          const uint32_t *off_t, const uint32_t *off_n, uint32_t *rt,
+                          uint32_t *rn, hipStream_t s);
+
+#endif

@@ -1,0 +1,101 @@
+"""CPU-only checks of the product library: it loads, exports every symbol the
+header declares, builds bit-exact host tables, and its host synthetic generator
+is deterministic.  No GPU compute here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# FNV-1a-64 of the reference's own tables (oracle/_ref/ref_harness tables).
+REF_HASHES = {"fk": "11bb85867221ee37", "coef": "86dcc255eecf756d", "lhet": "ff15c0af94a22f15"}
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "sniper_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ss_[a-z0-9_]+)\s*\(", src)) - {"ss_ctx"})
+
+
+def test_library_exports_every_header_symbol(pkg):
+    lib = pkg.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), f"missing export {s}"
+    assert set(syms) == set(pkg.EXPORTED_SYMBOLS)
+    assert lib.ss_abi_version() == 1
+
+
+def test_strerror_and_nodev(pkg):
+    lib = pkg.load_library()
+    assert b"ok" == lib.ss_strerror(0)
+    assert lib.ss_strerror(-5)
+
+
+def test_params_default_matches_reference_cli(pkg):
+    p = pkg.Params.default()
+    # sniper_maqcns.c:107-111 and main.c:70-78
+    assert abs(p.theta - 0.85) < 1e-7 and p.n_hap == 2 and abs(p.het_rate - 0.001) < 1e-9
+    assert abs(p.eta - 0.03) < 1e-8 and p.cap_mapQ == 60 and p.min_somatic_qual == 15
+    assert p.use_priors == 1 and p.use_joint_priors == 0 and p.somatic_rate == 0.01
+    assert p.include_loh == 1 and p.include_gor == 1
+
+
+def test_host_tables_match_reference_hashes(pkg):
+    h = pkg.model_check()
+    for k, v in REF_HASHES.items():
+        assert h[k] == v, k
+    assert abs(h["q_r"] - 26.9856968) < 1e-5
+
+
+def _fnv1a64(b: bytes) -> str:
+    h = 0xcbf29ce484222325
+    for x in b:
+        h = ((h ^ x) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return f"{h:016x}"
+
+
+def test_host_tables_match_oracle_for_nondefault(pkg, oracle):
+    """Non-default -T/-N/-r: no reference hash exists, so the product's host tables
+    are compared with the independently written oracle's (both pinned on the
+    defaults above)."""
+    p = pkg.Params.default(theta=0.9, n_hap=3, het_rate=0.01)
+    h = pkg.model_check(p)
+    t = oracle.Oracle(oracle.oparams(theta=0.9, n_hap=3, het_rate=0.01)).tables()
+    assert h["fk"] == _fnv1a64(t["fk"].tobytes())
+    assert h["lhet"] == _fnv1a64(t["lhet"].tobytes())
+    assert h["q_r"] == t["q_r"]
+
+
+def test_synth_host_deterministic_and_shaped(pkg):
+    s = pkg.Synth.default(60, 30)
+    a = pkg.synth_batch_host(s, 1000, 2000)
+    b = pkg.synth_batch_host(s, 1000, 2000)
+    for x, y in zip((a.ref, a.off_tumor, a.off_normal, a.reads_tumor, a.reads_normal),
+                    (b.ref, b.off_tumor, b.off_normal, b.reads_tumor, b.reads_normal)):
+        assert (x == y).all()
+    # windows are independent of batch boundaries (counter-based)
+    c = pkg.synth_batch_host(s, 1500, 500)
+    assert (c.ref == a.ref[500:1000]).all()
+    assert (c.reads_tumor == a.reads_tumor[a.off_tumor[500]:a.off_tumor[1000]]).all()
+    dt = np.diff(a.off_tumor.astype(np.int64))
+    dn = np.diff(a.off_normal.astype(np.int64))
+    assert 55 < dt.mean() < 63 and 27 < dn.mean() < 32
+    assert set(np.unique(a.ref).tolist()) <= set(b"ACGT")
+    mq = a.reads_tumor & 0xFF
+    assert 0.85 < (mq == 60).mean() < 0.95
+    bq = (a.reads_tumor >> 8) & 0xFF
+    assert bq.min() >= 2 and bq.max() <= 41
+
+
+def test_ctx_create_without_gpu_fails_loudly(pkg):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(pkg.SniperError) as e:
+        pkg.Context(pkg.Params.default())
+    assert e.value.code == pkg.SS_E_NODEV

@@ -1,0 +1,179 @@
+"""GPU parity: the HIP scorer (through the C ABI) against the CPU oracle.
+
+Bit-exact on every integer output of the reference path: glf_somatic's return
+value per site (somatic_sniper.c:109-273), both glf1_t records
+(sniper_maqcns.c:127-248) and every emitted call (its cns words, snp_q, joint
+genotypes, status).  The oracle itself is pinned to the compiled reference by
+tests/test_oracle_golden.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EXOTIC = dict(p_wild_qual=0.05, p_eq=0.02, p_iupac=0.02, p_nbase=0.02, p_ref_n=0.02,
+              p_ref_lower=0.05, p_ref_iupac=0.02, p_germline=0.03, p_somatic=0.05, vaf=0.4,
+              p_del=0.05)
+
+OPTSETS = [[], ["-J"], ["-p"], ["-s", "1e-6"], ["-T", "0.9", "-N", "3", "-r", "0.01"],
+           ["-Q", "0", "-L", "-G"], ["-J", "-p", "-Q", "0"], ["-L"], ["-G"]]
+
+
+def params_from_opts(pkg, opts):
+    p = pkg.Params.default()
+    it = iter(opts)
+    for o in it:
+        if o == "-T": p.theta = float(next(it))
+        elif o == "-N": p.n_hap = int(next(it))
+        elif o == "-r": p.het_rate = float(next(it))
+        elif o == "-p": p.use_priors = 0
+        elif o == "-J": p.use_joint_priors = 1
+        elif o == "-s": p.somatic_rate = float(next(it)); p.use_joint_priors = 1
+        elif o == "-Q": p.min_somatic_qual = int(next(it))
+        elif o == "-L": p.include_loh = 0
+        elif o == "-G": p.include_gor = 0
+    return p
+
+
+def assert_parity(pkg, oracle, batch, opts=(), ctx=None):
+    own = ctx is None
+    if own:
+        ctx = pkg.Context(params_from_opts(pkg, opts), device=0)
+    try:
+        score, calls, glf = ctx.score_batch(batch, want_glf=True)
+    finally:
+        if own:
+            ctx.close()
+    o = oracle.Oracle(oracle.opts_to_params(list(opts)))
+    o_score, o_calls, o_glf = o.score_batch(batch.ref, batch.off_tumor, batch.off_normal,
+                                            batch.reads_tumor, batch.reads_normal)
+    bad = np.nonzero(score != o_score)[0]
+    assert bad.size == 0, f"{bad.size} score mismatches, first {bad[:5]}: gpu {score[bad[:5]]} oracle {o_score[bad[:5]]}"
+    gb = glf.view(np.uint8).reshape(batch.n_sites, -1) != o_glf.view(np.uint8).reshape(batch.n_sites, -1)
+    bad = np.nonzero(gb.any(1))[0]
+    assert bad.size == 0, f"{bad.size} glf mismatches, first site {bad[0]}: gpu {glf[bad[0]]} oracle {o_glf[bad[0]]}"
+    assert len(calls) == len(o_calls)
+    assert (calls.view(np.uint8) == o_calls.view(np.uint8)).all()
+    return score, calls
+
+
+@pytest.mark.parametrize("lt,ln,kw", [(30, 30, {}), (60, 30, {}), (60, 30, EXOTIC), (100, 60, EXOTIC),
+                                      (3, 2, dict(p_wild_qual=0.3, p_del=0.3, p_somatic=0.1, p_germline=0.1))])
+@pytest.mark.parametrize("opts", OPTSETS)
+def test_synthetic_parity(pkg, oracle, lt, ln, kw, opts):
+    batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=1234 + lt, **kw), 0, 3000)
+    assert_parity(pkg, oracle, batch, opts)
+
+
+@pytest.mark.parametrize("lt,ln,fixed,n", [(300, 300, 0, 300), (700, 700, 1, 60), (500, 500, 0, 200),
+                                           (250, 270, 0, 400)])
+def test_deep_parity(pkg, oracle, ctx, lt, ln, fixed, n):
+    """Samples deeper than the main kernel's 256 -> deep kernel (LDS sort);
+    > 255 reads per class saturates w, > 255 total rescales c (Appendix A.4)."""
+    batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=fixed, **EXOTIC), 0, n)
+    assert_parity(pkg, oracle, batch, ctx=ctx)
+
+
+def test_giant_parity(pkg, oracle, ctx):
+    """> 4096 reads in a sample -> giant kernel with global scratch."""
+    big = pkg.synth_batch_host(pkg.Synth.default(6000, 4500, fixed_depth=1, **EXOTIC), 0, 6)
+    small = pkg.synth_batch_host(pkg.Synth.default(40, 40, **EXOTIC), 100, 20)
+    sites = [big.site(i) for i in range(big.n_sites)] + [small.site(i) for i in range(small.n_sites)]
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), ctx=ctx)
+
+
+def _r(pkg, mq, bq, nt, st):
+    return pkg.pack_read(mq, bq, nt, st)
+
+
+def quirk_sites(pkg):
+    R = lambda mq, bq, nt, st=0: _r(pkg, mq, bq, nt, st)
+    A, C_, G, T, N, EQ, M = 1, 2, 4, 8, 15, 0, 3
+    s = []
+    # Appendix A.1: N and IUPAC reads count as A; '=' resolves to the ref base
+    s.append(("C", [R(60, 30, N)] * 10, [R(60, 30, C_)] * 10))
+    s.append(("C", [R(60, 30, M)] * 10, [R(60, 30, C_)] * 10))
+    s.append(("G", [R(60, 30, EQ)] * 8 + [R(60, 30, T)] * 6, [R(60, 30, G)] * 9))
+    # A.2: q clamp; mapQ 0 reads still contribute with q=4; baseQ&0x3f==0 and min<4 drop
+    s.append(("A", [R(0, 30, T)] * 12 + [R(60, 30, A)] * 3, [R(60, 30, A)] * 12))
+    s.append(("A", [R(2, 64, T)] * 12 + [R(1, 128, T)] * 4 + [R(60, 30, A)] * 3, [R(60, 30, A)] * 12))
+    s.append(("A", [R(0, 0, T)] * 12 + [R(60, 30, A)] * 3, [R(60, 30, A)] * 12))
+    # A.3: mapQ >= 128 (rms uses mapQ & 0x7f), mapQ 255
+    s.append(("T", [R(200, 35, A, 1)] * 9 + [R(255, 20, T)] * 9, [R(130, 30, T)] * 9))
+    # depth 1 / all reads q==0 / all-deleted (empty packed list -> -1)
+    s.append(("A", [R(60, 30, C_)], [R(60, 30, A)]))
+    s.append(("A", [R(0, 0, C_)] * 3, [R(0, 0, A)] * 2))
+    s.append(("A", [], [R(60, 30, A)] * 5))
+    s.append(("A", [R(60, 30, A)] * 5, []))
+    # ref 'N' (skipped), ref 'n' (scored, never a candidate), IUPAC ref, '=' ref
+    s.append(("N", [R(60, 30, T)] * 10, [R(60, 30, A)] * 10))
+    s.append(("n", [R(60, 30, T)] * 10, [R(60, 30, A)] * 10))
+    s.append(("R", [R(60, 30, T)] * 10, [R(60, 30, A)] * 10))
+    s.append(("=", [R(60, 30, EQ)] * 10, [R(60, 30, A)] * 10))
+    s.append(("a", [R(60, 30, T)] * 10, [R(60, 30, A)] * 10))
+    # strong somatic, LOH, gain of reference, germline het
+    s.append(("A", [R(60, 35, T, i & 1) for i in range(20)], [R(60, 35, A, i & 1) for i in range(20)]))
+    s.append(("A", [R(60, 35, T)] * 20, [R(60, 35, A)] * 10 + [R(60, 35, T)] * 10))
+    s.append(("A", [R(60, 35, A)] * 10 + [R(60, 35, T)] * 10, [R(60, 35, T)] * 20))
+    s.append(("A", [R(60, 35, A)] * 10 + [R(60, 35, G)] * 10, [R(60, 35, A)] * 10 + [R(60, 35, G)] * 10))
+    # exactly 64 / 65 / 128 / 129 / 256 reads (register-sort boundaries), strands mixed
+    for n in (63, 64, 65, 127, 128, 129, 255, 256, 257):
+        s.append(("C", [R(60, 10 + (i * 7) % 31, C_ if i % 9 else G, i & 1) for i in range(n)],
+                  [R(60, 10 + (i * 5) % 31, C_, (i >> 1) & 1) for i in range(n // 2 + 1)]))
+    return s
+
+
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-Q", "0", "-L", "-G"], ["-p"]])
+def test_quirk_parity(pkg, oracle, opts):
+    batch = pkg.Batch.from_sites(quirk_sites(pkg))
+    score, _ = assert_parity(pkg, oracle, batch, opts)
+    assert score[9] == -1 and score[10] == -1     # empty packed sample
+    assert score[11] == -1                        # ref N
+    assert score[12] == 255                       # ref n: scored, not a candidate
+
+
+def test_device_synth_matches_host(pkg, ctx):
+    torch = pytest.importorskip("torch")
+    synth = pkg.Synth.default(60, 30, **EXOTIC)
+    d = ctx.synth_device(synth, 777, 5000)
+    h = pkg.synth_batch_host(synth, 777, 5000)
+    nt, nn = d["n_reads"]
+    assert nt == h.off_tumor[-1] and nn == h.off_normal[-1]
+    assert (d["ref"].cpu().numpy() == h.ref).all()
+    assert (d["off_tumor"].cpu().numpy().view(np.uint32) == h.off_tumor).all()
+    assert (d["off_normal"].cpu().numpy().view(np.uint32) == h.off_normal).all()
+    assert (d["reads_tumor"][:nt].cpu().numpy().view(np.uint32) == h.reads_tumor).all()
+    assert (d["reads_normal"][:nn].cpu().numpy().view(np.uint32) == h.reads_normal).all()
+
+
+def test_device_batch_full_size_properties(pkg, oracle, ctx):
+    """BASELINE workload shape (60x/30x) at 2M sites, HBM-resident: deterministic,
+    sampled windows bit-exact against the oracle, calls compacted correctly."""
+    torch = pytest.importorskip("torch")
+    n = 2_000_000
+    synth = pkg.Synth.default(60, 30)
+    d = ctx.synth_device(synth, 0, n)
+    dev = d["ref"].device
+    score = torch.empty(n, dtype=torch.int32, device=dev)
+    cap = 1 << 16
+    calls = torch.zeros(cap * 28, dtype=torch.uint8, device=dev)
+    ncalls = torch.zeros(1, dtype=torch.int32, device=dev)
+    args = (d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"])
+    ctx.score_device(*args, score=score, calls=calls, calls_cap=cap, n_calls=ncalls)
+    ctx.check()
+    s1 = score.cpu().numpy()
+    ctx.score_device(*args, score=score, calls=calls, calls_cap=cap, n_calls=ncalls)
+    ctx.check()
+    assert (score.cpu().numpy() == s1).all(), "non-deterministic"
+    k = int(ncalls.item())
+    c = calls.cpu().numpy()[: k * 28].view(pkg.SS_CALL_DTYPE)
+    assert len(np.unique(c["site"])) == k
+    assert set(np.unique(s1)) >= {255}
+    emitted = np.sort(c["site"])
+    for first in (0, 777_777, n - 4000):
+        h = pkg.synth_batch_host(synth, first, 4000)
+        o_score, o_calls, _ = oracle.Oracle().score_batch(h.ref, h.off_tumor, h.off_normal,
+                                                          h.reads_tumor, h.reads_normal, want_glf=False)
+        assert (s1[first:first + 4000] == o_score).all()
+        win = emitted[(emitted >= first) & (emitted < first + 4000)] - first
+        assert (win == o_calls["site"]).all()
