@@ -183,9 +183,14 @@ int  ss_score_batch_host(ss_ctx_t *ctx, const ss_batch_t *batch, const ss_out_t 
 int  ss_table_hashes(const ss_ctx_t *ctx, uint64_t *fk, uint64_t *coef,
                      uint64_t *lhet, float *q_r);
 /* Build the host tables for `p` without touching a GPU and report their hashes
- * (hashes[0..2] = fk, coef, lhet) and q_r.  Returns SS_E_TABLES when the
- * default-parameter tables differ from the pinned reference hashes. */
+ * (hashes[0..2] = fk, coef, lhet) and q_r.  The tables are built with this
+ * host's libm / x87 exactly as the reference builds them on this host (they are
+ * CPU-dependent in the reference too, see DESIGN.md "Tables").
+ * ss_model_pinned: 1 if hashes equal a recorded run of the compiled reference.
+ * With SS_STRICT_TABLES=1 in the environment, unpinned default tables make
+ * ss_model_check / ss_ctx_create fail with SS_E_TABLES. */
 int  ss_model_check(const ss_params_t *p, uint64_t hashes[3], float *q_r);
+int  ss_model_pinned(const uint64_t hashes[3]);
 /* Copy of the host tables (for tests): any pointer may be NULL. */
 int  ss_table_copy(const ss_ctx_t *ctx, double *fk, double *coef, double *lhet,
                    int *qadd1024, int *prior160, int *jprior1600);

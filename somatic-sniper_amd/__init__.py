@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "ss_abi_version", "ss_strerror", "ss_params_default", "ss_ctx_create", "ss_ctx_destroy",
     "ss_score_batch_device", "ss_score_batch_host", "ss_ctx_check", "ss_table_hashes",
     "ss_table_copy", "ss_synth_default", "ss_synth_batch_host", "ss_synth_batch_device",
-    "ss_set_kernel_timing", "ss_last_kernel_ms", "ss_kernel_time_log", "ss_model_check",
+    "ss_set_kernel_timing", "ss_last_kernel_ms", "ss_kernel_time_log", "ss_model_check", "ss_model_pinned",
 )
 
 
@@ -206,6 +206,7 @@ def load_library():
     lib.ss_last_kernel_ms.argtypes = [vp]
     lib.ss_last_kernel_ms.restype = C.c_double
     lib.ss_model_check.argtypes = [vp, vp, vp]
+    lib.ss_model_pinned.argtypes = [vp]
     lib.ss_kernel_time_log.argtypes = [vp, vp, C.c_int]
     if lib.ss_abi_version() != 1:
         raise RuntimeError("libsniper_amd.so ABI mismatch")
@@ -223,15 +224,16 @@ def _check(rc: int, what: str):
 
 
 def model_check(params: Params | None = None):
-    """Build the model tables on the host (no GPU needed) and return their hashes;
-    raises SniperError(SS_E_TABLES) if default-parameter tables differ from the
-    reference's (sniper_maqcns.c:27-100 on this host's libm)."""
+    """Build the model tables on the host (no GPU needed) and return their hashes and
+    whether they equal a recorded run of the compiled reference (sniper_maqcns.c:27-100
+    evaluated with this host's libm / x87, as the reference itself does)."""
     lib = load_library()
     p = params if params is not None else Params.default()
     h = (C.c_uint64 * 3)()
     qr = C.c_float()
     _check(lib.ss_model_check(C.byref(p), h, C.byref(qr)), "ss_model_check")
-    return {"fk": f"{h[0]:016x}", "coef": f"{h[1]:016x}", "lhet": f"{h[2]:016x}", "q_r": qr.value}
+    return {"fk": f"{h[0]:016x}", "coef": f"{h[1]:016x}", "lhet": f"{h[2]:016x}", "q_r": qr.value,
+            "pinned": bool(lib.ss_model_pinned(h))}
 
 
 def synth_batch_host(synth: Synth, first_site: int, n_sites: int) -> Batch:

@@ -22,6 +22,7 @@ typedef struct ss_host_model {
     int32_t  prior[16 * 10];
     int32_t  jprior[16 * 10 * 10];
     uint64_t h_fk, h_coef, h_lhet;
+    int      pinned;        /* default tables equal a pinned reference run */
 } ss_host_model_t;
 
 extern unsigned char ss_nt16_table[256];   /* valid after ss_host_model_build */

