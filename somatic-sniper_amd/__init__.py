@@ -186,6 +186,15 @@ def load_library():
     if not os.path.exists(path):
         raise RuntimeError(f"libsniper_amd.so not found at {path}: run __graft_entry__.build() "
                            f"(make -C somatic-sniper_amd); there is no CPU fallback")
+    if os.environ.get("SNIPER_AMD_NO_TORCH") != "1":
+        # One HIP runtime per process: PyTorch ships its own libamdhip64 with the
+        # same soname (libamdhip64.so.7).  Loading torch first makes our NEEDED
+        # entry bind to torch's copy, so device pointers and streams handed over
+        # from torch tensors live in the same runtime as our kernels.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = C.CDLL(path)
     vp, u64, u32 = C.c_void_p, C.c_uint64, C.c_uint32
     lib.ss_abi_version.restype = C.c_int
