@@ -227,6 +227,10 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.giant_scratch = c->d_giant_scratch;
     a.giant_keys = c->giant_keys;
     a.err = c->d_counters + 2;
+    {   /* profiling ablations only (DESIGN.md "Measurement"); never set in production */
+        const char *dg = getenv("SS_DIAG");
+        a.diag = dg ? (uint32_t)strtoul(dg, nullptr, 0) : 0u;
+    }
     a.m.fk = c->d_fk;
     a.m.coef = c->d_coef;
     a.m.lhet = c->d_lhet;

@@ -51,6 +51,7 @@ struct ss_score_args {
     uint32_t  *giant_scratch; /* [giant_blocks][2][giant_keys] */
     uint32_t   giant_keys;    /* keys per sample per giant block (power of two) */
     uint32_t  *err;           /* sticky error bits, see SS_KERR_* */
+    uint32_t   diag;          /* profiling ablations (SS_DIAG env), 0 in production */
     ss_dev_model m;
 };
 

@@ -31,7 +31,6 @@
 #include "ss_kernels.h"
 
 #define SENT 0xffffffffu
-#define ARENA 1024          /* sorted keys per wave (main kernel) */
 #define GMAX 8              /* sites per wave group               */
 
 namespace {
@@ -53,11 +52,17 @@ __device__ __forceinline__ uint32_t nt16_to_nt4(uint32_t b)
     return (b != 0u && (b & (b - 1u)) == 0u) ? (uint32_t)__builtin_ctz(b) : 4u;
 }
 
+/* Sum over the 64 lanes with DPP row shifts + row broadcasts (no LDS
+ * round trip); the total ends in lane 63 and is returned wave-uniform. */
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); /* row_shr:1 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); /* row_shr:2 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); /* row_shr:4 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); /* row_shr:8 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); /* row_bcast:15 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); /* row_bcast:31 */
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 /* --------------------------------------------------------------------------
@@ -153,7 +158,7 @@ struct SiteInfo {
 template <int K>
 __device__ __forceinline__ void sort_sample(const uint32_t *__restrict__ reads, uint32_t n,
                                             uint32_t ref16, uint32_t cap, uint32_t *arena,
-                                            SlotMeta &meta, uint32_t &nvalid)
+                                            SlotMeta &meta, uint32_t &nvalid, uint32_t diag)
 {
     const uint32_t lane = lane_id();
     uint32_t v[K];
@@ -168,7 +173,7 @@ __device__ __forceinline__ void sort_sample(const uint32_t *__restrict__ reads, 
             rs += t;
         }
     }
-    wave_bitonic<K>(v);
+    if (!(diag & 1u)) wave_bitonic<K>(v);
     uint32_t nv = 0, c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
     for (int r = 0; r < K; ++r) {
@@ -246,9 +251,58 @@ __device__ __forceinline__ int clamp_bar_e(float e, float f)
 
 /* --------------------------------------------------------------------------
  * Phase C: likelihoods + quantisation + consensus for one (site, sample)
- * (sniper_maqcns.c:176-248 and sniper_glf2cns :250-273).
+ * (sniper_maqcns.c:176-248 and sniper_glf2cns :250-273), computed by the
+ * 4 lanes of a quad: lane q evaluates genotypes {q, q+4, q+8} (upper-triangle
+ * order AA AC AG AT CC CG CT GG GT TT), then the 10 p values are exchanged
+ * with DPP quad broadcasts and every lane finishes redundantly.
  * ------------------------------------------------------------------------ */
-__device__ __forceinline__ void glf_and_cns(const float es[4], const float fs[4],
+__device__ __forceinline__ float quad_bcast(float v, int src)
+{
+    const int x = __builtin_bit_cast(int, v);
+    int r;
+    switch (src) {  /* quad_perm(src,src,src,src) */
+    case 0: r = __builtin_amdgcn_mov_dpp(x, 0x00, 0xf, 0xf, false); break;
+    case 1: r = __builtin_amdgcn_mov_dpp(x, 0x55, 0xf, 0xf, false); break;
+    case 2: r = __builtin_amdgcn_mov_dpp(x, 0xaa, 0xf, 0xf, false); break;
+    default: r = __builtin_amdgcn_mov_dpp(x, 0xff, 0xf, 0xf, false); break;
+    }
+    return __builtin_bit_cast(float, r);
+}
+
+/* genotype g -> alleles (j <= k) */
+__device__ __forceinline__ void geno_jk(int g, int &j, int &k)
+{
+    j = g < 4 ? 0 : (g < 7 ? 1 : (g < 9 ? 2 : 3));
+    k = g < 4 ? g : (g < 7 ? g - 3 : (g < 9 ? g - 5 : 3));
+}
+
+/* p for genotype (j,k) (sniper_maqcns.c:184-214); the sums skip {j,k} in
+ * ascending base order exactly like the reference's loops. */
+__device__ __forceinline__ float geno_p(int j, int k, const float es[4], const float fs[4],
+                                        const uint32_t c[4], uint32_t tot, const ss_dev_model &m)
+{
+    float e = 0.0f, f = 0.0f;
+    uint32_t c2 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bool use = i != j && i != k;
+        e = use ? e + es[i] : e;
+        f = use ? f + fs[i] : f;
+        c2 += use ? c[i] : 0u;
+    }
+    const bool hom = j == k;
+    const double lh = hom ? 0.0 : -4.343 * m.lhet[c[j] << 8 | c[k]];
+    float v;
+    if (c2) {
+        const double cf = m.coef[(uint32_t)clamp_bar_e(e, f) << 16 | tot << 8 | c2];
+        v = hom ? (float)((double)e + cf) : (float)((lh + (double)e) + cf);
+    } else {
+        v = hom ? 0.0f : (float)lh;
+    }
+    return v < 0.0f ? 0.0f : v;
+}
+
+__device__ __forceinline__ void glf_and_cns(int q, const float es[4], const float fs[4],
                                             const uint32_t craw[4], uint32_t n, uint64_t rms,
                                             const ss_dev_model &m, uint32_t lk[10],
                                             uint32_t &min_lk, uint32_t &rms_q, uint32_t &cns)
@@ -260,37 +314,18 @@ __device__ __forceinline__ void glf_and_cns(const float es[4], const float fs[4]
         for (int j = 0; j < 4; ++j) c[j] = (uint32_t)(int)(254.0 * (double)c[j] / (double)(int)tot + 0.5);
         tot = c[0] + c[1] + c[2] + c[3];
     }
-    /* p in upper-triangle order: AA AC AG AT CC CG CT GG GT TT */
-    float p[10];
-    /* index exactly as the reference: bar_e<<16 | c<<8 | tmp2 with OR -- after
-     * the rescale c may reach 256 and then aliases into the next bar_e row */
+    /* this lane's genotypes q, q+4, q+8 */
+    float mine[3];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int gjj = j == 0 ? 0 : (j == 1 ? 4 : (j == 2 ? 7 : 9));
-        {   /* homozygous j */
-            float e1 = 0.0f, f1 = 0.0f;
-            uint32_t c2 = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k != j) { e1 += es[k]; c2 += c[k]; f1 += fs[k]; }
-            float v = 0.0f;
-            if (c2) v = (float)((double)e1 + m.coef[(uint32_t)clamp_bar_e(e1, f1) << 16 | tot << 8 | c2]);
-            p[gjj] = v < 0.0f ? 0.0f : v;
-        }
-#pragma unroll
-        for (int k = j + 1; k < 4; ++k) {   /* heterozygous j/k */
-            float e2 = 0.0f, f2 = 0.0f;
-            uint32_t c3 = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (i != j && i != k) { e2 += es[i]; c3 += c[i]; f2 += fs[i]; }
-            const double lh = -4.343 * m.lhet[c[j] << 8 | c[k]];
-            float v;
-            if (c3) v = (float)((lh + (double)e2) + m.coef[(uint32_t)clamp_bar_e(e2, f2) << 16 | tot << 8 | c3]);
-            else v = (float)lh;
-            p[gjj + (k - j)] = v < 0.0f ? 0.0f : v;
-        }
+    for (int t = 0; t < 3; ++t) {
+        const int g = q + 4 * t;
+        int j, k;
+        geno_jk(g < 10 ? g : 9, j, k);
+        mine[t] = (g < 10) ? geno_p(j, k, es, fs, c, tot, m) : 0.0f;
     }
+    float p[10];
+#pragma unroll
+    for (int g = 0; g < 10; ++g) p[g] = quad_bcast(mine[g >> 2], g & 3);
     {   /* reduce the best-supported base's homozygote (:216-233) */
         float hi1 = -1.0f, hi2 = -1.0f, lo1 = 1e30f, lo2 = 1e30f;
         int hik = -1, lok = -1;
@@ -388,13 +423,16 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
     if (m.use_joint) {
         /* joint prior over (normal i, tumor j) with RAW glf lk (:180) */
         int marg = 255, best = 1000, bi = -1, bj = -1;
+#pragma unroll 1
         for (int i = 0; i < 10; ++i)
+#pragma unroll 1
             for (int j = 0; j < 10; ++j) {
                 int v = (int)rn.lk[i] + (int)rt.lk[j] + m.jprior[(rb4 * 10 + i) * 10 + j];
                 if (v > 255) v = 255;
                 if (v < best) { best = v; bi = i; bj = j; }
                 marg = qadd(m.qadd, marg, v, clamped);
             }
+#pragma unroll 1
         for (int j = 0; j < 10; ++j) {
             int v = (int)rn.lk[j] + (int)rt.lk[j] + m.jprior[(rb4 * 10 + j) * 10 + j];
             if (v > 255) v = 255;
@@ -407,18 +445,20 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
         jn = gb[bi];
         jt = gb[bj];
     } else {
-        /* calculatePosteriors (:79-99) for both samples, then the sum (:209-214) */
-        int lt[10], ln[10], st = 255, sn = 255;
+        /* calculatePosteriors (:79-99) for both samples, then the sum (:209-214);
+         * x_j is recomputed in the second pass instead of kept in an array */
+        int st = 255, sn = 255;
+#pragma unroll 1
         for (int j = 0; j < 10; ++j) {
             const int xt = (int)rt.lk[j] + m.prior[rb4 * 10 + j];
             const int xn = (int)rn.lk[j] + m.prior[rb4 * 10 + j];
             st = qadd(m.qadd, xt, st, clamped);
             sn = qadd(m.qadd, xn, sn, clamped);
-            lt[j] = xt;
-            ln[j] = xn;
         }
+#pragma unroll 1
         for (int j = 0; j < 10; ++j) {
-            int vt = lt[j] - st, vn = ln[j] - sn;
+            int vt = (int)rt.lk[j] + m.prior[rb4 * 10 + j] - st;
+            int vn = (int)rn.lk[j] + m.prior[rb4 * 10 + j] - sn;
             if (vt > 255) vt = 255;
             if (vn > 255) vn = 255;
             qps = qadd(m.qadd, qps, vt + vn, clamped);
@@ -480,22 +520,27 @@ __device__ __forceinline__ void finish_group(const ss_score_args &a, int G, cons
     float es = 0.0f, fs = 0.0f;
     if (s < G) {
         const SlotMeta &mt = meta[slot];
-        fold_group(keys_of(slot) + mt.start[b], mt.cnt[b], fk, es, fs);
+        if (!(a.diag & 2u)) fold_group(keys_of(slot) + mt.start[b], mt.cnt[b], fk, es, fs);
+        else { es = (float)mt.cnt[b]; fs = es; }
     }
-    /* gather the quad's four bases (all lanes active for the shuffles) */
+    /* gather the quad's four bases (all lanes active for the DPP moves) */
     float E[4], F[4];
-    const int q0 = (int)(lane & ~3u);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        E[i] = __shfl(es, q0 + i);
-        F[i] = __shfl(fs, q0 + i);
+        E[i] = quad_bcast(es, i);
+        F[i] = quad_bcast(fs, i);
     }
     if (s < G) {
         const SlotMeta &mt = meta[slot];
         const uint32_t cnt[4] = {mt.cnt[0], mt.cnt[1], mt.cnt[2], mt.cnt[3]};
         const uint64_t rms = (uint64_t)mt.rms_lo | (uint64_t)mt.rms_hi << 32;
         uint32_t lk[10], min_lk, rms_q, cns;
-        glf_and_cns(E, F, cnt, mt.n, rms, a.m, lk, min_lk, rms_q, cns);
+        if (!(a.diag & 4u)) glf_and_cns(b, E, F, cnt, mt.n, rms, a.m, lk, min_lk, rms_q, cns);
+        else {
+#pragma unroll
+            for (int g = 0; g < 10; ++g) lk[g] = (uint32_t)E[g & 3] & 0xffu;
+            min_lk = 0; rms_q = 0; cns = (uint32_t)F[0];
+        }
         if (b == 0) {
             SlotRes &r = res[slot];
 #pragma unroll
@@ -512,15 +557,34 @@ __device__ __forceinline__ void finish_group(const ss_score_args &a, int G, cons
         }
     }
     wave_sync();
-    if ((int)lane < G) decide_site(a, sinfo[lane].site, sinfo[lane].refc, res[2 * lane], res[2 * lane + 1]);
+    if ((int)lane < G) {
+        if (!(a.diag & 8u)) decide_site(a, sinfo[lane].site, sinfo[lane].refc, res[2 * lane], res[2 * lane + 1]);
+        else a.score[sinfo[lane].site] = (int32_t)res[2 * lane].cns;
+    }
     wave_sync();
 }
 
 /* --------------------------------------------------------------------------
  * Main kernel.
+ *
+ * Each wave walks 8-site BLOCKS (block b = sites [8b, 8b+8), grid-strided over
+ * waves).  A block's reads are contiguous in both CSR arrays, so a sub-group of
+ * its sites is staged into LDS with LDS-DMA (global_load_lds, no VGPRs) as two
+ * contiguous runs: [tumor reads | normal reads].  Two staging buffers per wave
+ * form a software pipeline: the DMA of the NEXT sub-group is issued right after
+ * phase A of the current one and lands while the current one folds (phase B
+ * has no VMEM, so nothing forces an early drain).  The staged reads are sorted
+ * in place, so the staging buffer is also the sorted-key arena of phase B.
+ * The block descriptor (offsets + ref chars of the 8 sites) lives in one VGPR
+ * and is prefetched one block ahead.
  * ------------------------------------------------------------------------ */
+#define STG 1024            /* staged u32 per buffer (per wave) */
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void glb_void_t;
+
 struct MainLds {
-    uint32_t arena[4][ARENA];
+    uint32_t stage[4][2][STG];
     SlotMeta meta[4][2 * GMAX];
     SlotRes  res[4][2 * GMAX];
     SiteInfo sinfo[4][GMAX];
@@ -528,11 +592,85 @@ struct MainLds {
 
 __device__ __forceinline__ void phase_a_sample(const uint32_t *reads, uint32_t n, uint32_t ref16,
                                                uint32_t cap, uint32_t *arena, SlotMeta &meta,
-                                               uint32_t &nv)
+                                               uint32_t &nv, uint32_t diag)
 {
-    if (n <= 64u) sort_sample<1>(reads, n, ref16, cap, arena, meta, nv);
-    else if (n <= 128u) sort_sample<2>(reads, n, ref16, cap, arena, meta, nv);
-    else sort_sample<4>(reads, n, ref16, cap, arena, meta, nv);
+    if (n <= 64u) sort_sample<1>(reads, n, ref16, cap, arena, meta, nv, diag);
+    else if (n <= 128u) sort_sample<2>(reads, n, ref16, cap, arena, meta, nv, diag);
+    else sort_sample<4>(reads, n, ref16, cap, arena, meta, nv, diag);
+}
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+/* lanes 0..8: off_t[s..s+8], lanes 16..24: off_n[s..s+8], lanes 32..39: ref[s..s+7] */
+__device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s)
+{
+    const uint32_t lane = lane_id();
+    uint32_t v = 0;
+    if (lane < 9u) {
+        if (s + lane <= a.n_sites) v = a.off_t[s + lane];
+    } else if (lane >= 16u && lane < 25u) {
+        if (s + (lane - 16u) <= a.n_sites) v = a.off_n[s + (lane - 16u)];
+    } else if (lane >= 32u && lane < 40u) {
+        if (s + (lane - 32u) < a.n_sites) v = a.ref[s + (lane - 32u)];
+    }
+    return v;
+}
+
+__device__ __forceinline__ void push_deep(const ss_score_args &a, uint32_t site)
+{
+    if (lane_id() == 0) {
+        const uint32_t d = atomicAdd(a.deep_count, 1u);
+        if (d < a.deep_cap) a.deep_list[d] = site;
+        else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
+    }
+}
+
+struct Sub {
+    uint32_t a, b;        /* site range [a, b) within the block */
+    uint32_t t0, lt;      /* tumor read run  */
+    uint32_t n0, ln;      /* normal read run */
+};
+
+/* Largest run of sites from `pos` whose reads fit one staging buffer.  A site
+ * that alone exceeds it is deep by construction and goes to the deep list. */
+__device__ __forceinline__ Sub form_sub(const ss_score_args &a, uint32_t desc, uint32_t nsite,
+                                        uint32_t pos, uint64_t sblk)
+{
+    uint32_t i = pos, tot = 0;
+    while (i < nsite) {
+        const uint32_t sz = (rl(desc, i + 1u) - rl(desc, i)) + (rl(desc, i + 17u) - rl(desc, i + 16u));
+        if (sz > STG) {
+            if (i == pos) { push_deep(a, (uint32_t)(sblk + i)); pos = ++i; continue; }
+            break;
+        }
+        if (tot + sz > STG) break;
+        tot += sz;
+        ++i;
+    }
+    Sub r;
+    r.a = pos;
+    r.b = i;
+    r.t0 = rl(desc, pos);
+    r.lt = rl(desc, i) - r.t0;
+    r.n0 = rl(desc, pos + 16u);
+    r.ln = rl(desc, i + 16u) - r.n0;
+    return r;
+}
+
+__device__ __forceinline__ void issue_dma(const ss_score_args &a, const Sub &r, uint32_t *buf)
+{
+    const uint32_t lane = lane_id();
+    for (uint32_t i = 0; i < r.lt; i += 64u)
+        if (i + lane < r.lt)
+            __builtin_amdgcn_global_load_lds((glb_void_t *)(a.reads_t + r.t0 + i + lane),
+                                             (lds_void_t *)(buf + i), 4, 0, 0);
+    for (uint32_t i = 0; i < r.ln; i += 64u)
+        if (i + lane < r.ln)
+            __builtin_amdgcn_global_load_lds((glb_void_t *)(a.reads_n + r.n0 + i + lane),
+                                             (lds_void_t *)(buf + r.lt + i), 4, 0, 0);
 }
 
 }  // namespace
@@ -546,49 +684,83 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = a.m.fk[i];
     __syncthreads();
 
-    uint32_t *arena = L.arena[wv];
     SlotMeta *meta = L.meta[wv];
     SlotRes *res = L.res[wv];
     SiteInfo *sinfo = L.sinfo[wv];
     const uint64_t nwaves = (uint64_t)gridDim.x * (SS_MAIN_BLOCK / 64);
+    const uint64_t nblocks = (a.n_sites + GMAX - 1) / GMAX;
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
 
-    for (uint64_t g = (uint64_t)blockIdx.x * (SS_MAIN_BLOCK / 64) + wv; g * GMAX < a.n_sites; g += nwaves) {
-        uint64_t s = g * GMAX;
-        const uint64_t end = s + GMAX < a.n_sites ? s + GMAX : a.n_sites;
-        while (s < end) {
-            int G = 0;
-            uint32_t used = 0;
-            /* ---- phase A: sort the group's samples into the arena ---- */
-            for (; s < end; ++s) {
-                const uint32_t ot = a.off_t[s], nt = a.off_t[s + 1] - ot;
-                const uint32_t on = a.off_n[s], nn = a.off_n[s + 1] - on;
-                if (nt > SS_MAIN_MAXN || nn > SS_MAIN_MAXN) {
-                    if (lane == 0) {
-                        const uint32_t d = atomicAdd(a.deep_count, 1u);
-                        if (d < a.deep_cap) a.deep_list[d] = (uint32_t)s;
-                        else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
-                    }
-                    continue;
-                }
-                if (used + nt + nn > ARENA) break;   /* arena full: finish this group first */
-                const uint32_t refc = a.ref[s];
-                const uint32_t ref16 = a.m.nt16[refc];
-                uint32_t nv;
-                if (lane == 0) { sinfo[G].site = (uint32_t)s; sinfo[G].refc = refc; }
-                if (lane == 0) meta[2 * G].base = used;
-                phase_a_sample(a.reads_t + ot, nt, ref16, cap, arena + used, meta[2 * G], nv);
-                used += nv;
-                if (lane == 0) meta[2 * G + 1].base = used;
-                phase_a_sample(a.reads_n + on, nn, ref16, cap, arena + used, meta[2 * G + 1], nv);
-                used += nv;
-                ++G;
+    /* ---- prologue: first non-empty sub-group, its DMA, next descriptor ---- */
+    uint64_t blk = (uint64_t)blockIdx.x * (SS_MAIN_BLOCK / 64) + wv;
+    if (blk >= nblocks) return;
+    uint32_t desc = load_desc(a, blk * GMAX);
+    uint32_t nsite = (uint32_t)(a.n_sites - blk * GMAX < GMAX ? a.n_sites - blk * GMAX : GMAX);
+    Sub cur = form_sub(a, desc, nsite, 0, blk * GMAX);
+    uint64_t nblk = blk + nwaves;
+    uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GMAX) : 0u;
+    while (cur.a == cur.b) {               /* whole block deep */
+        blk = nblk;
+        if (blk >= nblocks) return;
+        desc = ndesc;
+        nsite = (uint32_t)(a.n_sites - blk * GMAX < GMAX ? a.n_sites - blk * GMAX : GMAX);
+        nblk = blk + nwaves;
+        ndesc = nblk < nblocks ? load_desc(a, nblk * GMAX) : 0u;
+        cur = form_sub(a, desc, nsite, 0, blk * GMAX);
+    }
+    uint32_t c = 0;
+    issue_dma(a, cur, L.stage[wv][0]);
+
+    for (;;) {
+        uint32_t *stage = L.stage[wv][c];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* this sub-group's DMA has landed */
+        /* ---- phase A: sort the sub-group's samples in place ---- */
+        int G = 0;
+        for (uint32_t i = cur.a; i < cur.b; ++i) {
+            const uint32_t site = (uint32_t)(blk * GMAX + i);
+            const uint32_t t_i = rl(desc, i), nt = rl(desc, i + 1u) - t_i;
+            const uint32_t n_i = rl(desc, i + 16u), nn = rl(desc, i + 17u) - n_i;
+            if (nt > SS_MAIN_MAXN || nn > SS_MAIN_MAXN) { push_deep(a, site); continue; }
+            const uint32_t refc = rl(desc, i + 32u) & 0xffu;
+            const uint32_t ref16 = a.m.nt16[refc];
+            const uint32_t bt = t_i - cur.t0, bn = cur.lt + (n_i - cur.n0);
+            uint32_t nv;
+            if (lane == 0) {
+                sinfo[G].site = site;
+                sinfo[G].refc = refc;
+                meta[2 * G].base = bt;
+                meta[2 * G + 1].base = bn;
             }
-            wave_sync();
-            if (G > 0)
-                finish_group(a, G, meta, res, sinfo, fk,
-                             [&](int slot) -> const uint32_t * { return arena + meta[slot].base; });
+            phase_a_sample(stage + bt, nt, ref16, cap, stage + bt, meta[2 * G], nv, a.diag);
+            phase_a_sample(stage + bn, nn, ref16, cap, stage + bn, meta[2 * G + 1], nv, a.diag);
+            ++G;
         }
+        /* ---- next sub-group: same block, else the next non-empty block ---- */
+        Sub nxt;
+        bool have = false;
+        if (cur.b < nsite) {
+            nxt = form_sub(a, desc, nsite, cur.b, blk * GMAX);
+            have = nxt.a < nxt.b;
+        }
+        while (!have) {
+            blk = nblk;
+            if (blk >= nblocks) break;
+            desc = ndesc;
+            nsite = (uint32_t)(a.n_sites - blk * GMAX < GMAX ? a.n_sites - blk * GMAX : GMAX);
+            nblk = blk + nwaves;
+            ndesc = nblk < nblocks ? load_desc(a, nblk * GMAX) : 0u;
+            nxt = form_sub(a, desc, nsite, 0, blk * GMAX);
+            have = nxt.a < nxt.b;
+        }
+        if (have) issue_dma(a, nxt, L.stage[wv][c ^ 1u]);
+        /* ---- phases B, C, D (the DMA above lands meanwhile) ---- */
+        wave_sync();
+        if (G > 0)
+            finish_group(a, G, meta, res, sinfo, fk,
+                         [&](int slot) -> const uint32_t * { return stage + meta[slot].base; });
+        if (!have) break;
+        cur = nxt;
+        c ^= 1u;
     }
 }
 
