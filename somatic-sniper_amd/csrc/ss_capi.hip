@@ -244,9 +244,12 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.m.use_joint = c->hm.prm.use_joint_priors;
     a.m.include_loh = c->hm.prm.include_loh;
     a.m.include_gor = c->hm.prm.include_gor;
-    const uint64_t groups = (b->n_sites + 7) / 8;
-    uint64_t blocks = (groups + 3) / 4;
-    const uint64_t max_blocks = (uint64_t)c->n_cu * 32;
+    /* main kernel: 4 waves per workgroup, one 16-site block per wave per
+     * iteration, grid-strided; 4 workgroups fit a CU (LDS), so 16 per CU gives
+     * each CU four rounds of waves for load balance */
+    const uint64_t site_blocks = (b->n_sites + 15) / 16;
+    uint64_t blocks = (site_blocks + 3) / 4;
+    const uint64_t max_blocks = (uint64_t)c->n_cu * 16;
     if (blocks > max_blocks) blocks = max_blocks;
     const int deep_grid = c->n_cu * 4;
     c->last_stream = s;

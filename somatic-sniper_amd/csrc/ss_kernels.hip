@@ -31,7 +31,7 @@
 #include "ss_kernels.h"
 
 #define SENT 0xffffffffu
-#define GMAX 8              /* sites per wave group               */
+#define GMAX 8              /* sites per group (deep kernel finish)  */
 
 namespace {
 
@@ -302,30 +302,26 @@ __device__ __forceinline__ float geno_p(int j, int k, const float es[4], const f
     return v < 0.0f ? 0.0f : v;
 }
 
-__device__ __forceinline__ void glf_and_cns(int q, const float es[4], const float fs[4],
-                                            const uint32_t craw[4], uint32_t n, uint64_t rms,
-                                            const ss_dev_model &m, uint32_t lk[10],
-                                            uint32_t &min_lk, uint32_t &rms_q, uint32_t &cns)
+/* counts rescale of sniper_maqcns.c:178-182 */
+__device__ __forceinline__ uint32_t rescale_counts(const uint32_t craw[4], uint32_t c[4])
 {
-    uint32_t c[4] = {craw[0], craw[1], craw[2], craw[3]};
-    uint32_t tot = c[0] + c[1] + c[2] + c[3];
+    uint32_t tot = craw[0] + craw[1] + craw[2] + craw[3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = craw[j];
     if (tot > 255u) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) c[j] = (uint32_t)(int)(254.0 * (double)c[j] / (double)(int)tot + 0.5);
         tot = c[0] + c[1] + c[2] + c[3];
     }
-    /* this lane's genotypes q, q+4, q+8 */
-    float mine[3];
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-        const int g = q + 4 * t;
-        int j, k;
-        geno_jk(g < 10 ? g : 9, j, k);
-        mine[t] = (g < 10) ? geno_p(j, k, es, fs, c, tot, m) : 0.0f;
-    }
-    float p[10];
-#pragma unroll
-    for (int g = 0; g < 10; ++g) p[g] = quad_bcast(mine[g >> 2], g & 3);
+    return tot;
+}
+
+/* hom fix, quantisation and glf2cns from the 10 genotype p values
+ * (sniper_maqcns.c:216-244, sniper_glf2cns :250-273). */
+__device__ __forceinline__ void glf_finish(float p[10], const float es[4], uint32_t n, uint64_t rms,
+                                           const ss_dev_model &m, uint32_t lk[10],
+                                           uint32_t &min_lk, uint32_t &rms_q, uint32_t &cns)
+{
     {   /* reduce the best-supported base's homozygote (:216-233) */
         float hi1 = -1.0f, hi2 = -1.0f, lo1 = 1e30f, lo2 = 1e30f;
         int hik = -1, lok = -1;
@@ -382,6 +378,47 @@ __device__ __forceinline__ void glf_and_cns(int q, const float es[4], const floa
     x |= b2 < 10000 ? (uint32_t)(b2 - b1 < 256 ? b2 - b1 : 255) << 8 : 0xffu << 8;
     x |= (b2 < 10000 && b3 < 10000) ? (uint32_t)(b3 - b2 < 256 ? b3 - b2 : 255) : 0xffu;
     cns = x;
+}
+
+/* quad-cooperative version (deep kernel): lane q of the quad evaluates
+ * genotypes {q, q+4, q+8}, DPP quad broadcasts exchange them. */
+__device__ __forceinline__ void glf_and_cns(int q, const float es[4], const float fs[4],
+                                            const uint32_t craw[4], uint32_t n, uint64_t rms,
+                                            const ss_dev_model &m, uint32_t lk[10],
+                                            uint32_t &min_lk, uint32_t &rms_q, uint32_t &cns)
+{
+    uint32_t c[4];
+    const uint32_t tot = rescale_counts(craw, c);
+    float mine[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int g = q + 4 * t;
+        int j, k;
+        geno_jk(g < 10 ? g : 9, j, k);
+        mine[t] = (g < 10) ? geno_p(j, k, es, fs, c, tot, m) : 0.0f;
+    }
+    float p[10];
+#pragma unroll
+    for (int g = 0; g < 10; ++g) p[g] = quad_bcast(mine[g >> 2], g & 3);
+    glf_finish(p, es, n, rms, m, lk, min_lk, rms_q, cns);
+}
+
+/* single-lane version (main kernel: one lane per (site, sample)) */
+__device__ __forceinline__ void glf_and_cns_lane(const float es[4], const float fs[4],
+                                                 const uint32_t craw[4], uint32_t n, uint64_t rms,
+                                                 const ss_dev_model &m, uint32_t lk[10],
+                                                 uint32_t &min_lk, uint32_t &rms_q, uint32_t &cns)
+{
+    uint32_t c[4];
+    const uint32_t tot = rescale_counts(craw, c);
+    float p[10];
+#pragma unroll
+    for (int g = 0; g < 10; ++g) {
+        int j, k;
+        geno_jk(g, j, k);
+        p[g] = geno_p(j, k, es, fs, c, tot, m);
+    }
+    glf_finish(p, es, n, rms, m, lk, min_lk, rms_q, cns);
 }
 
 /* qAdd (somatic_sniper.c:18) with the out-of-range index clamped + counted */
@@ -567,36 +604,307 @@ __device__ __forceinline__ void finish_group(const ss_score_args &a, int G, cons
 /* --------------------------------------------------------------------------
  * Main kernel.
  *
- * Each wave walks 8-site BLOCKS (block b = sites [8b, 8b+8), grid-strided over
- * waves).  A block's reads are contiguous in both CSR arrays, so a sub-group of
- * its sites is staged into LDS with LDS-DMA (global_load_lds, no VGPRs) as two
- * contiguous runs: [tumor reads | normal reads].  Two staging buffers per wave
- * form a software pipeline: the DMA of the NEXT sub-group is issued right after
- * phase A of the current one and lands while the current one folds (phase B
- * has no VMEM, so nothing forces an early drain).  The staged reads are sorted
- * in place, so the staging buffer is also the sorted-key arena of phase B.
- * The block descriptor (offsets + ref chars of the 8 sites) lives in one VGPR
- * and is prefetched one block ahead.
+ * A wave walks 16-site BLOCKS (grid-strided).  A block's reads are contiguous
+ * in both CSR arrays, so a run of its sites ("sub-group") is staged into LDS
+ * with LDS-DMA (global_load_lds, no VGPRs) as [tumor reads | normal reads];
+ * the DMA of the next sub-group is issued after this one's fold and lands
+ * while the likelihood/decision phases run.
+ *
+ * Phase A, per site: ONE wave-wide bitonic sort of 16-bit keys packed two per
+ * VGPR covers both samples (sample bit on top):
+ *   sample<<15 | base<<13 | minq<<5 | hasbase<<4 | strand<<3 | t
+ * where t in 0..6 encodes baseQ relative to 64/128/192 when minq < 4 (the only
+ * case where the reference's baseQ tie-break changes the clamped q, see
+ * read_key16) and 0 otherwise.  Inside one (sample, base) group the reference's
+ * descending key walk visits elements in exactly this order up to swaps of
+ * elements with identical (q, strand), which leave every float sum unchanged.
+ * Sorted keys are turned into 16-bit fold records (q | strand<<8) and written
+ * back over the site's own staged reads (tumor records into its tumor run,
+ * normal records into its normal run).
+ *
+ * Phases B+C: lane (site, sample) walks its sample's four base groups (longest
+ * first, so the wave-wide trip count is set by one long chain per lane) and
+ * then evaluates the 10 genotypes.  Phase D: lane s decides site s.
  * ------------------------------------------------------------------------ */
-#define STG 1024            /* staged u32 per buffer (per wave) */
+#define GB 16               /* sites per block                 */
+#define STG 2048            /* staged u32 per wave             */
+#define PK_MAX 512          /* nT + nN handled by the packed sort (K <= 4) */
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void glb_void_t;
 
-struct MainLds {
-    uint32_t stage[4][2][STG];
-    SlotMeta meta[4][2 * GMAX];
-    SlotRes  res[4][2 * GMAX];
-    SiteInfo sinfo[4][GMAX];
+struct Slot3 {
+    uint32_t rec_n;      /* u16 index of the fold records | non-deleted depth << 16 */
+    uint32_t cnt01;      /* cnt[0] | cnt[1] << 16 */
+    uint32_t cnt23;      /* cnt[2] | cnt[3] << 16 */
+    uint32_t rms;        /* sum of min(mapQ & 0x7f, cap)^2 */
 };
 
-__device__ __forceinline__ void phase_a_sample(const uint32_t *reads, uint32_t n, uint32_t ref16,
-                                               uint32_t cap, uint32_t *arena, SlotMeta &meta,
-                                               uint32_t &nv, uint32_t diag)
+struct Res3 {
+    uint32_t lk[3];      /* 10 bytes packed */
+    uint32_t cns;
+    uint32_t depth;
+};
+
+struct MainLds {
+    uint32_t stage[4][STG];
+    Slot3    slot[4][2 * GB];
+    Res3     res[4][2 * GB];
+    uint32_t site[4][GB];
+    uint32_t refc[4][GB];
+};
+
+/* 16-bit order key (see the section comment); 0xffff = no contribution. */
+__device__ __forceinline__ uint32_t read_key16(uint32_t rd, uint32_t ref16, uint32_t sample)
 {
-    if (n <= 64u) sort_sample<1>(reads, n, ref16, cap, arena, meta, nv, diag);
-    else if (n <= 128u) sort_sample<2>(reads, n, ref16, cap, arena, meta, nv, diag);
-    else sort_sample<4>(reads, n, ref16, cap, arena, meta, nv, diag);
+    const uint32_t mq = rd & 0xffu, bq = (rd >> 8) & 0xffu;
+    const uint32_t nt = (rd >> 16) & 0xfu, st = (rd >> 20) & 1u;
+    const uint32_t minq = mq < bq ? mq : bq;
+    const bool valid = minq != 0u || (bq & 0x3fu) != 0u;
+    const uint32_t nt4 = nt16_to_nt4(nt ? nt : ref16);
+    const uint32_t hb = nt4 < 4u ? 1u : 0u;
+    const uint32_t base = hb ? nt4 : 0u;
+    uint32_t t = 0;
+    if (minq < 4u)
+        t = (bq >= 64u) + (bq > 64u) + (bq >= 128u) + (bq > 128u) + (bq >= 192u) + (bq > 192u);
+    return valid ? (sample << 15 | base << 13 | minq << 5 | hb << 4 | st << 3 | t) : 0xffffu;
+}
+
+/* fold record of a sorted key: clamped q (sniper_maqcns.c:165) | strand << 8 */
+__device__ __forceinline__ uint32_t key_to_rec(uint32_t k)
+{
+    const uint32_t minq = (k >> 5) & 0xffu, st = (k >> 3) & 1u, weird = k & 1u;
+    const uint32_t q = (minq < 4u && !weird) ? 4u : minq;
+    return q | st << 8;
+}
+
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b)
+{
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const us2 x = __builtin_bit_cast(us2, a), y = __builtin_bit_cast(us2, b);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(x, y));
+}
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b)
+{
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const us2 x = __builtin_bit_cast(us2, a), y = __builtin_bit_cast(us2, b);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
+}
+
+/* x from lane ^ LJ without an LDS round trip: DPP quad permutes for 1 and 2,
+ * DPP row shifts for 4 and 8, v_permlane16/32_swap for 16 and 32. */
+template <int LJ>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x)
+{
+    const int xi = (int)x;
+    if constexpr (LJ == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0xb1, 0xf, 0xf, false);  /* quad_perm 1,0,3,2 */
+    } else if constexpr (LJ == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x4e, 0xf, 0xf, false);  /* quad_perm 2,3,0,1 */
+    } else if constexpr (LJ == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x104, 0xf, 0xf, false); /* row_shl:4 */
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x114, 0xf, 0xf, false); /* row_shr:4 */
+        return (lane_id() & 4u) ? dn : up;
+    } else if constexpr (LJ == 8) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x108, 0xf, 0xf, false); /* row_shl:8 */
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x118, 0xf, 0xf, false); /* row_shr:8 */
+        return (lane_id() & 8u) ? dn : up;
+    } else if constexpr (LJ == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane_id() & 16u) ? r[0] : r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane_id() & 32u) ? r[0] : r[1];
+    }
+}
+
+__device__ __forceinline__ uint32_t xor_lane_dyn(uint32_t x, int lj)
+{
+    switch (lj) {
+    case 1: return xor_lane<1>(x);
+    case 2: return xor_lane<2>(x);
+    case 4: return xor_lane<4>(x);
+    case 8: return xor_lane<8>(x);
+    case 16: return xor_lane<16>(x);
+    default: return xor_lane<32>(x);
+    }
+}
+
+/* Bitonic sort, ascending, of 128*K u16 keys: element e = lane*2K + 2r + h
+ * lives in half h of v[r]. */
+template <int K>
+__device__ __forceinline__ void packed_bitonic(uint32_t (&v)[K])
+{
+    const uint32_t lane = lane_id();
+    constexpr uint32_t E = 2u * K;          /* elements per lane */
+#pragma unroll
+    for (uint32_t k = 2; k <= 128u * K; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            if (j >= E) {                   /* across lanes */
+                const int lj = (int)(j / E);
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    const uint32_t e = lane * E + 2u * r;
+                    const uint32_t o = xor_lane_dyn(v[r], lj);   /* lj is a constant after unrolling */
+                    const bool up = (e & k) == 0u, lower = (e & j) == 0u;
+                    const uint32_t mn = pk_min(v[r], o), mx = pk_max(v[r], o);
+                    v[r] = (lower == up) ? mn : mx;
+                }
+            } else if (j >= 2u) {           /* across registers of a lane */
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    const int r2 = r ^ (int)(j >> 1);
+                    if (r2 > r) {
+                        const uint32_t e = lane * E + 2u * r;
+                        const bool up = (e & k) == 0u;
+                        const uint32_t mn = pk_min(v[r], v[r2]), mx = pk_max(v[r], v[r2]);
+                        v[r] = up ? mn : mx;
+                        v[r2] = up ? mx : mn;
+                    }
+                }
+            } else {                        /* the two halves of a register */
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    const uint32_t e = lane * E + 2u * r;
+                    const bool up = (e & k) == 0u;
+                    const uint32_t sw = (v[r] >> 16) | (v[r] << 16);
+                    const uint32_t mn = pk_min(v[r], sw), mx = pk_max(v[r], sw);
+                    v[r] = up ? ((mn & 0xffffu) | (mx & 0xffff0000u)) : ((mx & 0xffffu) | (mn & 0xffff0000u));
+                }
+            }
+        }
+    }
+}
+
+/* number of u16 keys (both halves of all K registers) below x, wave-wide */
+template <int K>
+__device__ __forceinline__ uint32_t count_below(const uint32_t (&v)[K], uint32_t x)
+{
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        c += (uint32_t)__popcll(__ballot((v[r] & 0xffffu) < x));
+        c += (uint32_t)__popcll(__ballot((v[r] >> 16) < x));
+    }
+    return c;
+}
+
+/* Phase A for one site: stage_t / stage_n hold the site's staged reads; the
+ * fold records are written back over them (u16 view). */
+template <int K>
+__device__ __forceinline__ void sort_site(uint32_t *stage, uint32_t bt, uint32_t nt, uint32_t bn,
+                                          uint32_t nn, uint32_t ref16, uint32_t cap,
+                                          Slot3 &st_t, Slot3 &st_n, uint32_t diag)
+{
+    const uint32_t lane = lane_id();
+    uint32_t v[K];
+    uint32_t rs_t = 0, rs_n = 0;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t e = ((uint32_t)r * 64u + lane) * 2u + (uint32_t)h;   /* input placement */
+            uint32_t key = 0xffffu;
+            if (e < nt + nn) {
+                const bool tum = e < nt;
+                const uint32_t rd = stage[tum ? bt + e : bn + (e - nt)];
+                uint32_t t = rd & 0x7fu;
+                t = t < cap ? t : cap;
+                if (tum) rs_t += t * t; else rs_n += t * t;
+                key = read_key16(rd, ref16, tum ? 0u : 1u);
+            }
+            w |= key << (16 * h);
+        }
+        v[r] = w;
+    }
+    if (!(diag & 1u)) packed_bitonic<K>(v);
+    /* group boundaries (sample, base) */
+    const uint32_t c1 = count_below<K>(v, 1u << 13), c2 = count_below<K>(v, 2u << 13);
+    const uint32_t c3 = count_below<K>(v, 3u << 13), c4 = count_below<K>(v, 4u << 13);
+    const uint32_t c5 = count_below<K>(v, 5u << 13), c6 = count_below<K>(v, 6u << 13);
+    const uint32_t c7 = count_below<K>(v, 7u << 13), c8 = count_below<K>(v, 0xffffu);
+    /* fold records back over the staged reads: tumor run, normal run */
+    uint16_t *rec = reinterpret_cast<uint16_t *>(stage);
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
+            const uint32_t key = (v[r] >> (16 * h)) & 0xffffu;
+            if (e < c8) {
+                const uint32_t idx = e < c4 ? 2u * bt + e : 2u * bn + (e - c4);
+                rec[idx] = (uint16_t)key_to_rec(key);
+            }
+        }
+    }
+    const uint32_t rms_t = wave_sum(rs_t), rms_n = wave_sum(rs_n);
+    if (lane == 0) {
+        st_t.rec_n = 2u * bt | nt << 16;
+        st_t.cnt01 = c1 | (c2 - c1) << 16;
+        st_t.cnt23 = (c3 - c2) | (c4 - c3) << 16;
+        st_t.rms = rms_t;
+        st_n.rec_n = 2u * bn | nn << 16;
+        st_n.cnt01 = (c5 - c4) | (c6 - c5) << 16;
+        st_n.cnt23 = (c7 - c6) | (c8 - c7) << 16;
+        st_n.rms = rms_n;
+    }
+}
+
+/* one ordered fold step (sniper_maqcns.c:165-172) on a record */
+__device__ __forceinline__ void fold_step(uint32_t rc, const double *fk, float &es, float &fs,
+                                          uint32_t &w0, uint32_t &w1)
+{
+    const uint32_t q = rc & 0xffu, st = rc >> 8;
+    const uint32_t w = st ? w1 : w0;
+    const double f = fk[w];
+    es = (float)((double)es + f * (double)q);
+    fs = (float)((double)fs + f);
+    const uint32_t wn = w < 255u ? w + 1u : 255u;
+    if (st) w1 = wn; else w0 = wn;
+}
+
+/* Fold of one (site, sample): its four base groups, the longest first. */
+__device__ __forceinline__ void fold_sample(const uint16_t *rec, const uint32_t cnt[4],
+                                            const double *fk, float es[4], float fs[4])
+{
+    uint32_t start[4], order[4];
+    start[0] = 0;
+    start[1] = cnt[0];
+    start[2] = cnt[0] + cnt[1];
+    start[3] = start[2] + cnt[2];
+    /* longest group first, the rest in base order */
+    uint32_t L = 0;
+#pragma unroll
+    for (int b = 1; b < 4; ++b) L = cnt[b] > cnt[L] ? (uint32_t)b : L;
+    order[0] = L;
+    {
+        int o = 1;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b)
+            if (b != L) order[o++] = b;
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) { es[b] = 0.0f; fs[b] = 0.0f; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t b = order[i];
+        const uint32_t s0 = b == 0 ? start[0] : (b == 1 ? start[1] : (b == 2 ? start[2] : start[3]));
+        uint32_t t = b == 0 ? cnt[0] : (b == 1 ? cnt[1] : (b == 2 ? cnt[2] : cnt[3]));
+        float e = 0.0f, f = 0.0f;
+        uint32_t w0 = 0, w1 = 0;
+        uint32_t nxt = t ? rec[s0 + t - 1] : 0u;
+        while (t) {
+            --t;
+            const uint32_t cur = nxt;
+            if (t) nxt = rec[s0 + t - 1];
+            fold_step(cur, fk, e, f, w0, w1);
+        }
+#pragma unroll
+        for (uint32_t bb = 0; bb < 4; ++bb)
+            if (bb == b) { es[bb] = e; fs[bb] = f; }
+    }
 }
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
@@ -604,20 +912,26 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
-/* lanes 0..8: off_t[s..s+8], lanes 16..24: off_n[s..s+8], lanes 32..39: ref[s..s+7] */
+/* lanes 0..16: off_t[s..s+16], 17..32: ref[s..s+15], 33..49: off_n[s..s+16] */
 __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s)
 {
     const uint32_t lane = lane_id();
     uint32_t v = 0;
-    if (lane < 9u) {
+    if (lane < 17u) {
         if (s + lane <= a.n_sites) v = a.off_t[s + lane];
-    } else if (lane >= 16u && lane < 25u) {
-        if (s + (lane - 16u) <= a.n_sites) v = a.off_n[s + (lane - 16u)];
-    } else if (lane >= 32u && lane < 40u) {
-        if (s + (lane - 32u) < a.n_sites) v = a.ref[s + (lane - 32u)];
+    } else if (lane < 33u) {
+        if (s + (lane - 17u) < a.n_sites) {
+            const uint32_t rc = a.ref[s + (lane - 17u)];
+            v = rc | (uint32_t)a.m.nt16[rc] << 8;
+        }
+    } else if (lane < 50u) {
+        if (s + (lane - 33u) <= a.n_sites) v = a.off_n[s + (lane - 33u)];
     }
     return v;
 }
+#define D_T(i) rl(desc, (i))
+#define D_REF(i) rl(desc, 17u + (i))
+#define D_N(i) rl(desc, 33u + (i))
 
 __device__ __forceinline__ void push_deep(const ss_score_args &a, uint32_t site)
 {
@@ -634,15 +948,15 @@ struct Sub {
     uint32_t n0, ln;      /* normal read run */
 };
 
-/* Largest run of sites from `pos` whose reads fit one staging buffer.  A site
- * that alone exceeds it is deep by construction and goes to the deep list. */
+/* Largest run of sites from `pos` whose reads fit one staging buffer; a site
+ * too deep for the packed sort is left to the deep kernel. */
 __device__ __forceinline__ Sub form_sub(const ss_score_args &a, uint32_t desc, uint32_t nsite,
                                         uint32_t pos, uint64_t sblk)
 {
     uint32_t i = pos, tot = 0;
     while (i < nsite) {
-        const uint32_t sz = (rl(desc, i + 1u) - rl(desc, i)) + (rl(desc, i + 17u) - rl(desc, i + 16u));
-        if (sz > STG) {
+        const uint32_t sz = (D_T(i + 1u) - D_T(i)) + (D_N(i + 1u) - D_N(i));
+        if (sz > PK_MAX) {
             if (i == pos) { push_deep(a, (uint32_t)(sblk + i)); pos = ++i; continue; }
             break;
         }
@@ -653,10 +967,10 @@ __device__ __forceinline__ Sub form_sub(const ss_score_args &a, uint32_t desc, u
     Sub r;
     r.a = pos;
     r.b = i;
-    r.t0 = rl(desc, pos);
-    r.lt = rl(desc, i) - r.t0;
-    r.n0 = rl(desc, pos + 16u);
-    r.ln = rl(desc, i + 16u) - r.n0;
+    r.t0 = D_T(pos);
+    r.lt = D_T(i) - r.t0;
+    r.n0 = D_N(pos);
+    r.ln = D_N(i) - r.n0;
     return r;
 }
 
@@ -673,6 +987,73 @@ __device__ __forceinline__ void issue_dma(const ss_score_args &a, const Sub &r, 
                                              (lds_void_t *)(buf + r.lt + i), 4, 0, 0);
 }
 
+/* Phases B, C, D for the G sites of a sub-group. */
+__device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32_t *stage,
+                                           const Slot3 *slot, Res3 *res, const uint32_t *sites,
+                                           const uint32_t *refcs, const double *fk,
+                                           bool have_next, const Sub &nxt)
+{
+    const uint32_t lane = lane_id();
+    const int sl = (int)lane;                      /* slot = site * 2 + sample */
+    float es[4], fs[4];
+    uint32_t cnt[4];
+    if (sl < 2 * G) {
+        const Slot3 &m3 = slot[sl];
+        cnt[0] = m3.cnt01 & 0xffffu; cnt[1] = m3.cnt01 >> 16;
+        cnt[2] = m3.cnt23 & 0xffffu; cnt[3] = m3.cnt23 >> 16;
+        const uint16_t *rec = reinterpret_cast<const uint16_t *>(stage) + (m3.rec_n & 0xffffu);
+        if (!(a.diag & 2u)) fold_sample(rec, cnt, fk, es, fs);
+        else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) { es[b] = (float)cnt[b]; fs[b] = es[b]; }
+        }
+    }
+    /* every fold record has been read: the next sub-group's reads may now
+     * stream into the stage while the likelihoods are computed */
+    wave_sync();
+    if (have_next) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue_dma(a, nxt, stage);
+    }
+    if (sl < 2 * G) {
+        const Slot3 &m3 = slot[sl];
+        uint32_t lk[10], min_lk, rms_q, cns;
+        const uint32_t depth = m3.rec_n >> 16;
+        if (!(a.diag & 4u)) glf_and_cns_lane(es, fs, cnt, depth, m3.rms, a.m, lk, min_lk, rms_q, cns);
+        else {
+#pragma unroll
+            for (int g = 0; g < 10; ++g) lk[g] = (uint32_t)es[g & 3] & 0xffu;
+            min_lk = 0; rms_q = 0; cns = (uint32_t)fs[0];
+        }
+        Res3 &r = res[sl];
+        r.lk[0] = lk[0] | lk[1] << 8 | lk[2] << 16 | lk[3] << 24;
+        r.lk[1] = lk[4] | lk[5] << 8 | lk[6] << 16 | lk[7] << 24;
+        r.lk[2] = lk[8] | lk[9] << 8;
+        r.cns = cns;
+        r.depth = depth;
+        if (a.glf) {
+            const uint32_t s = (uint32_t)sl >> 1;
+            store_glf(&a.glf[2ull * sites[s] + (sl & 1)], a.m.nt16[refcs[s] & 0xffu], lk, min_lk,
+                      rms_q, r.depth);
+        }
+    }
+    wave_sync();
+    if ((int)lane < G) {
+        const Res3 &rt = res[2 * lane], &rn = res[2 * lane + 1];
+        SlotRes t, n;
+#pragma unroll
+        for (int g = 0; g < 10; ++g) {
+            t.lk[g] = (uint8_t)(rt.lk[g >> 2] >> (8 * (g & 3)));
+            n.lk[g] = (uint8_t)(rn.lk[g >> 2] >> (8 * (g & 3)));
+        }
+        t.cns = rt.cns; t.depth = rt.depth;
+        n.cns = rn.cns; n.depth = rn.depth;
+        if (!(a.diag & 8u)) decide_site(a, sites[lane], refcs[lane], t, n);
+        else a.score[sites[lane]] = (int32_t)rt.cns;
+    }
+    wave_sync();
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
@@ -684,83 +1065,72 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = a.m.fk[i];
     __syncthreads();
 
-    SlotMeta *meta = L.meta[wv];
-    SlotRes *res = L.res[wv];
-    SiteInfo *sinfo = L.sinfo[wv];
+    uint32_t *stage = L.stage[wv];
+    Slot3 *slot = L.slot[wv];
+    Res3 *res = L.res[wv];
+    uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
     const uint64_t nwaves = (uint64_t)gridDim.x * (SS_MAIN_BLOCK / 64);
-    const uint64_t nblocks = (a.n_sites + GMAX - 1) / GMAX;
+    const uint64_t nblocks = (a.n_sites + GB - 1) / GB;
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
 
-    /* ---- prologue: first non-empty sub-group, its DMA, next descriptor ---- */
     uint64_t blk = (uint64_t)blockIdx.x * (SS_MAIN_BLOCK / 64) + wv;
     if (blk >= nblocks) return;
-    uint32_t desc = load_desc(a, blk * GMAX);
-    uint32_t nsite = (uint32_t)(a.n_sites - blk * GMAX < GMAX ? a.n_sites - blk * GMAX : GMAX);
-    Sub cur = form_sub(a, desc, nsite, 0, blk * GMAX);
+    uint32_t desc = load_desc(a, blk * GB);
+    uint32_t nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
     uint64_t nblk = blk + nwaves;
-    uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GMAX) : 0u;
+    uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
+    Sub cur = form_sub(a, desc, nsite, 0, blk * GB);
     while (cur.a == cur.b) {               /* whole block deep */
         blk = nblk;
         if (blk >= nblocks) return;
         desc = ndesc;
-        nsite = (uint32_t)(a.n_sites - blk * GMAX < GMAX ? a.n_sites - blk * GMAX : GMAX);
+        nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
         nblk = blk + nwaves;
-        ndesc = nblk < nblocks ? load_desc(a, nblk * GMAX) : 0u;
-        cur = form_sub(a, desc, nsite, 0, blk * GMAX);
+        ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
+        cur = form_sub(a, desc, nsite, 0, blk * GB);
     }
-    uint32_t c = 0;
-    issue_dma(a, cur, L.stage[wv][0]);
+    issue_dma(a, cur, stage);
 
     for (;;) {
-        uint32_t *stage = L.stage[wv][c];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* this sub-group's DMA has landed */
-        /* ---- phase A: sort the sub-group's samples in place ---- */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the sub-group's reads are in LDS */
+        /* ---- phase A ---- */
         int G = 0;
         for (uint32_t i = cur.a; i < cur.b; ++i) {
-            const uint32_t site = (uint32_t)(blk * GMAX + i);
-            const uint32_t t_i = rl(desc, i), nt = rl(desc, i + 1u) - t_i;
-            const uint32_t n_i = rl(desc, i + 16u), nn = rl(desc, i + 17u) - n_i;
-            if (nt > SS_MAIN_MAXN || nn > SS_MAIN_MAXN) { push_deep(a, site); continue; }
-            const uint32_t refc = rl(desc, i + 32u) & 0xffu;
-            const uint32_t ref16 = a.m.nt16[refc];
+            const uint32_t site = (uint32_t)(blk * GB + i);
+            const uint32_t t_i = D_T(i), nt = D_T(i + 1u) - t_i;
+            const uint32_t n_i = D_N(i), nn = D_N(i + 1u) - n_i;
+            const uint32_t rdesc = D_REF(i);
+            const uint32_t refc = rdesc & 0xffu, ref16 = rdesc >> 8;
             const uint32_t bt = t_i - cur.t0, bn = cur.lt + (n_i - cur.n0);
-            uint32_t nv;
-            if (lane == 0) {
-                sinfo[G].site = site;
-                sinfo[G].refc = refc;
-                meta[2 * G].base = bt;
-                meta[2 * G + 1].base = bn;
-            }
-            phase_a_sample(stage + bt, nt, ref16, cap, stage + bt, meta[2 * G], nv, a.diag);
-            phase_a_sample(stage + bn, nn, ref16, cap, stage + bn, meta[2 * G + 1], nv, a.diag);
+            if (lane == 0) { sites[G] = site; refcs[G] = refc; }
+            const uint32_t tot = nt + nn;
+            if (tot <= 128u) sort_site<1>(stage, bt, nt, bn, nn, ref16, cap, slot[2 * G], slot[2 * G + 1], a.diag);
+            else if (tot <= 256u) sort_site<2>(stage, bt, nt, bn, nn, ref16, cap, slot[2 * G], slot[2 * G + 1], a.diag);
+            else sort_site<4>(stage, bt, nt, bn, nn, ref16, cap, slot[2 * G], slot[2 * G + 1], a.diag);
             ++G;
         }
+        wave_sync();
         /* ---- next sub-group: same block, else the next non-empty block ---- */
         Sub nxt;
         bool have = false;
         if (cur.b < nsite) {
-            nxt = form_sub(a, desc, nsite, cur.b, blk * GMAX);
+            nxt = form_sub(a, desc, nsite, cur.b, blk * GB);
             have = nxt.a < nxt.b;
         }
         while (!have) {
             blk = nblk;
             if (blk >= nblocks) break;
             desc = ndesc;
-            nsite = (uint32_t)(a.n_sites - blk * GMAX < GMAX ? a.n_sites - blk * GMAX : GMAX);
+            nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
             nblk = blk + nwaves;
-            ndesc = nblk < nblocks ? load_desc(a, nblk * GMAX) : 0u;
-            nxt = form_sub(a, desc, nsite, 0, blk * GMAX);
+            ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
+            nxt = form_sub(a, desc, nsite, 0, blk * GB);
             have = nxt.a < nxt.b;
         }
-        if (have) issue_dma(a, nxt, L.stage[wv][c ^ 1u]);
-        /* ---- phases B, C, D (the DMA above lands meanwhile) ---- */
-        wave_sync();
-        if (G > 0)
-            finish_group(a, G, meta, res, sinfo, fk,
-                         [&](int slot) -> const uint32_t * { return stage + meta[slot].base; });
+        /* ---- phases B + C + D (the next DMA is issued after the fold) ---- */
+        finish_sub(a, G, stage, slot, res, sites, refcs, fk, have, nxt);
         if (!have) break;
         cur = nxt;
-        c ^= 1u;
     }
 }
 
