@@ -712,9 +712,20 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
     } else if constexpr (LJ == 16) {
         const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
         return (lane_id() & 16u) ? r[0] : r[1];
-    } else {
+    } else if constexpr (LJ == 32) {
         const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
         return (lane_id() & 32u) ? r[0] : r[1];
+    } else if constexpr (LJ == 3) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x1b, 0xf, 0xf, false);   /* quad_perm 3,2,1,0 */
+    } else if constexpr (LJ == 7) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x141, 0xf, 0xf, false);  /* row_half_mirror */
+    } else if constexpr (LJ == 15) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x140, 0xf, 0xf, false);  /* row_mirror */
+    } else if constexpr (LJ == 31) {
+        return xor_lane<16>(xor_lane<15>(x));
+    } else {
+        static_assert(LJ == 63, "unsupported lane xor");
+        return xor_lane<32>(xor_lane<31>(x));
     }
 }
 
@@ -777,6 +788,103 @@ __device__ __forceinline__ void packed_bitonic(uint32_t (&v)[K])
     }
 }
 
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane_m(uint32_t x) { return xor_lane<M>(x); }
+
+__device__ __forceinline__ uint32_t halfswap(uint32_t x) { return (x >> 16) | (x << 16); }
+
+/* Bitonic sort (the "flip" formulation: every comparator puts the minimum at
+ * the lower index, so all directions are single lane bits), ascending, of
+ * 128*K u16 keys: element e = lane*2K + 2r + h lives in half h of v[r]. */
+/* half cleaners e <-> e ^ j for j = J, J/2, ..., 1 (compile-time recursion) */
+template <int K, uint32_t J>
+__device__ __forceinline__ void half_clean(uint32_t (&v)[K])
+{
+    constexpr uint32_t E = 2u * K;
+    if constexpr (J == 0) {
+        return;
+    } else {
+        if constexpr (J >= E) {
+            constexpr uint32_t lj = J / E;
+            const bool lower = (lane_id() & lj) == 0u;
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                const uint32_t o = xor_lane<(int)lj>(v[r]);
+                v[r] = lower ? pk_min(v[r], o) : pk_max(v[r], o);
+            }
+        } else if constexpr (J >= 2u) {
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                const int r2 = r ^ (int)(J >> 1);
+                if (r2 > r) {
+                    const uint32_t mn = pk_min(v[r], v[r2]), mx = pk_max(v[r], v[r2]);
+                    v[r] = mn;
+                    v[r2] = mx;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                const uint32_t sw = halfswap(v[r]);
+                const uint32_t mn = pk_min(v[r], sw), mx = pk_max(v[r], sw);
+                v[r] = (mn & 0xffffu) | (mx & 0xffff0000u);
+            }
+        }
+        half_clean<K, (J >> 1)>(v);
+    }
+}
+
+template <int K, uint32_t k>
+__device__ __forceinline__ void flip_stage(uint32_t (&v)[K])
+{
+    constexpr uint32_t E = 2u * K;
+    const uint32_t lane = lane_id();
+    /* mirror: e <-> e ^ (k-1) */
+    if constexpr (k <= E) {
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            const int i1 = (2 * r) ^ (int)(k - 1);
+            const int r2 = i1 >> 1;
+            if (r2 > r) {
+                const uint32_t sw = halfswap(v[r2]);
+                const uint32_t mn = pk_min(v[r], sw), mx = pk_max(v[r], sw);
+                v[r] = mn;
+                v[r2] = halfswap(mx);
+            } else if (r2 == r) {
+                const uint32_t sw = halfswap(v[r]);
+                const uint32_t mn = pk_min(v[r], sw), mx = pk_max(v[r], sw);
+                v[r] = (mn & 0xffffu) | (mx & 0xffff0000u);
+            }
+        }
+    } else {
+        constexpr uint32_t m = k / E - 1u;              /* lane xor of the mirror */
+        const bool lower = (lane & ((m + 1u) >> 1)) == 0u;
+        uint32_t nv[K];
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            const uint32_t o = halfswap(xor_lane_m<(int)m>(v[K - 1 - r]));
+            nv[r] = lower ? pk_min(v[r], o) : pk_max(v[r], o);
+        }
+#pragma unroll
+        for (int r = 0; r < K; ++r) v[r] = nv[r];
+    }
+    half_clean<K, (k >> 2)>(v);
+}
+
+template <int K>
+__device__ __forceinline__ void packed_bitonic_flip(uint32_t (&v)[K])
+{
+    flip_stage<K, 2>(v);
+    flip_stage<K, 4>(v);
+    flip_stage<K, 8>(v);
+    flip_stage<K, 16>(v);
+    flip_stage<K, 32>(v);
+    flip_stage<K, 64>(v);
+    flip_stage<K, 128>(v);
+    if constexpr (K >= 2) flip_stage<K, 256>(v);
+    if constexpr (K >= 4) flip_stage<K, 512>(v);
+}
+
 /* number of u16 keys (both halves of all K registers) below x, wave-wide */
 template <int K>
 __device__ __forceinline__ uint32_t count_below(const uint32_t (&v)[K], uint32_t x)
@@ -819,7 +927,7 @@ __device__ __forceinline__ void sort_site(uint32_t *stage, uint32_t bt, uint32_t
         }
         v[r] = w;
     }
-    if (!(diag & 1u)) packed_bitonic<K>(v);
+    if (!(diag & 1u)) packed_bitonic_flip<K>(v);
     /* group boundaries (sample, base) */
     const uint32_t c1 = count_below<K>(v, 1u << 13), c2 = count_below<K>(v, 2u << 13);
     const uint32_t c3 = count_below<K>(v, 3u << 13), c4 = count_below<K>(v, 4u << 13);
