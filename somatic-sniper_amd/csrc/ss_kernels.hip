@@ -788,17 +788,17 @@ __device__ __forceinline__ void packed_bitonic(uint32_t (&v)[K])
     }
 }
 
-template <int M>
-__device__ __forceinline__ uint32_t xor_lane_m(uint32_t x) { return xor_lane<M>(x); }
 
 __device__ __forceinline__ uint32_t halfswap(uint32_t x) { return (x >> 16) | (x << 16); }
 
 /* Bitonic sort (the "flip" formulation: every comparator puts the minimum at
  * the lower index, so all directions are single lane bits), ascending, of
  * 128*K u16 keys: element e = lane*2K + 2r + h lives in half h of v[r]. */
-/* half cleaners e <-> e ^ j for j = J, J/2, ..., 1 (compile-time recursion) */
-template <int K, uint32_t J>
-__device__ __forceinline__ void half_clean(uint32_t (&v)[K])
+/* half cleaners e <-> e ^ j for j = J, J/2, ..., 1 (compile-time recursion);
+ * M independent networks are advanced together so their dependency chains
+ * (and DPP wait states) interleave. */
+template <int M, int K, uint32_t J>
+__device__ __forceinline__ void half_clean(uint32_t (&v)[M][K])
 {
     constexpr uint32_t E = 2u * K;
     if constexpr (J == 0) {
@@ -808,81 +808,94 @@ __device__ __forceinline__ void half_clean(uint32_t (&v)[K])
             constexpr uint32_t lj = J / E;
             const bool lower = (lane_id() & lj) == 0u;
 #pragma unroll
-            for (int r = 0; r < K; ++r) {
-                const uint32_t o = xor_lane<(int)lj>(v[r]);
-                v[r] = lower ? pk_min(v[r], o) : pk_max(v[r], o);
-            }
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    const uint32_t o = xor_lane<(int)lj>(v[m][r]);
+                    v[m][r] = lower ? pk_min(v[m][r], o) : pk_max(v[m][r], o);
+                }
         } else if constexpr (J >= 2u) {
 #pragma unroll
-            for (int r = 0; r < K; ++r) {
-                const int r2 = r ^ (int)(J >> 1);
-                if (r2 > r) {
-                    const uint32_t mn = pk_min(v[r], v[r2]), mx = pk_max(v[r], v[r2]);
-                    v[r] = mn;
-                    v[r2] = mx;
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    const int r2 = r ^ (int)(J >> 1);
+                    if (r2 > r) {
+                        const uint32_t mn = pk_min(v[m][r], v[m][r2]), mx = pk_max(v[m][r], v[m][r2]);
+                        v[m][r] = mn;
+                        v[m][r2] = mx;
+                    }
                 }
-            }
         } else {
 #pragma unroll
-            for (int r = 0; r < K; ++r) {
-                const uint32_t sw = halfswap(v[r]);
-                const uint32_t mn = pk_min(v[r], sw), mx = pk_max(v[r], sw);
-                v[r] = (mn & 0xffffu) | (mx & 0xffff0000u);
-            }
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    const uint32_t sw = halfswap(v[m][r]);
+                    const uint32_t mn = pk_min(v[m][r], sw), mx = pk_max(v[m][r], sw);
+                    v[m][r] = (mn & 0xffffu) | (mx & 0xffff0000u);
+                }
         }
-        half_clean<K, (J >> 1)>(v);
+        half_clean<M, K, (J >> 1)>(v);
     }
 }
 
-template <int K, uint32_t k>
-__device__ __forceinline__ void flip_stage(uint32_t (&v)[K])
+/* Bitonic sort (the "flip" formulation: every comparator puts the minimum at
+ * the lower index, so all directions are single lane bits), ascending, of
+ * 128*K u16 keys: element e = lane*2K + 2r + h lives in half h of v[m][r]. */
+template <int M, int K, uint32_t k>
+__device__ __forceinline__ void flip_stage(uint32_t (&v)[M][K])
 {
     constexpr uint32_t E = 2u * K;
     const uint32_t lane = lane_id();
     /* mirror: e <-> e ^ (k-1) */
     if constexpr (k <= E) {
 #pragma unroll
-        for (int r = 0; r < K; ++r) {
-            const int i1 = (2 * r) ^ (int)(k - 1);
-            const int r2 = i1 >> 1;
-            if (r2 > r) {
-                const uint32_t sw = halfswap(v[r2]);
-                const uint32_t mn = pk_min(v[r], sw), mx = pk_max(v[r], sw);
-                v[r] = mn;
-                v[r2] = halfswap(mx);
-            } else if (r2 == r) {
-                const uint32_t sw = halfswap(v[r]);
-                const uint32_t mn = pk_min(v[r], sw), mx = pk_max(v[r], sw);
-                v[r] = (mn & 0xffffu) | (mx & 0xffff0000u);
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                const int r2 = ((2 * r) ^ (int)(k - 1)) >> 1;
+                if (r2 > r) {
+                    const uint32_t sw = halfswap(v[m][r2]);
+                    const uint32_t mn = pk_min(v[m][r], sw), mx = pk_max(v[m][r], sw);
+                    v[m][r] = mn;
+                    v[m][r2] = halfswap(mx);
+                } else if (r2 == r) {
+                    const uint32_t sw = halfswap(v[m][r]);
+                    const uint32_t mn = pk_min(v[m][r], sw), mx = pk_max(v[m][r], sw);
+                    v[m][r] = (mn & 0xffffu) | (mx & 0xffff0000u);
+                }
             }
-        }
     } else {
-        constexpr uint32_t m = k / E - 1u;              /* lane xor of the mirror */
-        const bool lower = (lane & ((m + 1u) >> 1)) == 0u;
-        uint32_t nv[K];
+        constexpr uint32_t mx_lane = k / E - 1u;          /* lane xor of the mirror */
+        const bool lower = (lane & ((mx_lane + 1u) >> 1)) == 0u;
 #pragma unroll
-        for (int r = 0; r < K; ++r) {
-            const uint32_t o = halfswap(xor_lane_m<(int)m>(v[K - 1 - r]));
-            nv[r] = lower ? pk_min(v[r], o) : pk_max(v[r], o);
+        for (int m = 0; m < M; ++m) {
+            uint32_t nv[K];
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                const uint32_t o = halfswap(xor_lane<(int)mx_lane>(v[m][K - 1 - r]));
+                nv[r] = lower ? pk_min(v[m][r], o) : pk_max(v[m][r], o);
+            }
+#pragma unroll
+            for (int r = 0; r < K; ++r) v[m][r] = nv[r];
         }
-#pragma unroll
-        for (int r = 0; r < K; ++r) v[r] = nv[r];
     }
-    half_clean<K, (k >> 2)>(v);
+    half_clean<M, K, (k >> 2)>(v);
 }
 
-template <int K>
-__device__ __forceinline__ void packed_bitonic_flip(uint32_t (&v)[K])
+template <int M, int K>
+__device__ __forceinline__ void packed_bitonic_flip(uint32_t (&v)[M][K])
 {
-    flip_stage<K, 2>(v);
-    flip_stage<K, 4>(v);
-    flip_stage<K, 8>(v);
-    flip_stage<K, 16>(v);
-    flip_stage<K, 32>(v);
-    flip_stage<K, 64>(v);
-    flip_stage<K, 128>(v);
-    if constexpr (K >= 2) flip_stage<K, 256>(v);
-    if constexpr (K >= 4) flip_stage<K, 512>(v);
+    flip_stage<M, K, 2>(v);
+    flip_stage<M, K, 4>(v);
+    flip_stage<M, K, 8>(v);
+    flip_stage<M, K, 16>(v);
+    flip_stage<M, K, 32>(v);
+    flip_stage<M, K, 64>(v);
+    flip_stage<M, K, 128>(v);
+    if constexpr (K >= 2) flip_stage<M, K, 256>(v);
+    if constexpr (K >= 4) flip_stage<M, K, 512>(v);
 }
 
 /* number of u16 keys (both halves of all K registers) below x, wave-wide */
@@ -898,120 +911,129 @@ __device__ __forceinline__ uint32_t count_below(const uint32_t (&v)[K], uint32_t
     return c;
 }
 
-/* Phase A for one site: stage_t / stage_n hold the site's staged reads; the
- * fold records are written back over them (u16 view). */
-template <int K>
-__device__ __forceinline__ void sort_site(uint32_t *stage, uint32_t bt, uint32_t nt, uint32_t bn,
-                                          uint32_t nn, uint32_t ref16, uint32_t cap,
-                                          Slot3 &st_t, Slot3 &st_n, uint32_t diag)
+/* Phase A for M sites at once (independent networks interleaved): each
+ * site's staged reads are keyed, sorted, and its fold records are written
+ * back over them (u16 view); slot[2m], slot[2m+1] receive its bookkeeping. */
+struct SiteA {
+    uint32_t bt, nt, bn, nn, ref16;
+};
+
+template <int K, int M>
+__device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M], uint32_t cap,
+                                           Slot3 *slot, uint32_t diag)
 {
     const uint32_t lane = lane_id();
-    uint32_t v[K];
-    uint32_t rs_t = 0, rs_n = 0;
+    uint32_t v[M][K];
+    uint32_t rs_t[M], rs_n[M];
 #pragma unroll
-    for (int r = 0; r < K; ++r) {
-        uint32_t w = 0;
+    for (int m = 0; m < M; ++m) {
+        rs_t[m] = 0;
+        rs_n[m] = 0;
+        const uint32_t nt = S[m].nt, nn = S[m].nn;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t e = ((uint32_t)r * 64u + lane) * 2u + (uint32_t)h;   /* input placement */
-            uint32_t key = 0xffffu;
-            if (e < nt + nn) {
-                const bool tum = e < nt;
-                const uint32_t rd = stage[tum ? bt + e : bn + (e - nt)];
-                uint32_t t = rd & 0x7fu;
-                t = t < cap ? t : cap;
-                if (tum) rs_t += t * t; else rs_n += t * t;
-                key = read_key16(rd, ref16, tum ? 0u : 1u);
+        for (int r = 0; r < K; ++r) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t e = ((uint32_t)r * 64u + lane) * 2u + (uint32_t)h;   /* input placement */
+                uint32_t key = 0xffffu;
+                if (e < nt + nn) {
+                    const bool tum = e < nt;
+                    const uint32_t rd = stage[tum ? S[m].bt + e : S[m].bn + (e - nt)];
+                    uint32_t t = rd & 0x7fu;
+                    t = t < cap ? t : cap;
+                    if (tum) rs_t[m] += t * t; else rs_n[m] += t * t;
+                    key = (diag & 16u) ? ((rd & 0x7fffu) | (tum ? 0u : 0x8000u))
+                                       : read_key16(rd, S[m].ref16, tum ? 0u : 1u);
+                }
+                w |= key << (16 * h);
             }
-            w |= key << (16 * h);
+            v[m][r] = w;
         }
-        v[r] = w;
     }
-    if (!(diag & 1u)) packed_bitonic_flip<K>(v);
-    /* group boundaries (sample, base) */
-    const uint32_t c1 = count_below<K>(v, 1u << 13), c2 = count_below<K>(v, 2u << 13);
-    const uint32_t c3 = count_below<K>(v, 3u << 13), c4 = count_below<K>(v, 4u << 13);
-    const uint32_t c5 = count_below<K>(v, 5u << 13), c6 = count_below<K>(v, 6u << 13);
-    const uint32_t c7 = count_below<K>(v, 7u << 13), c8 = count_below<K>(v, 0xffffu);
-    /* fold records back over the staged reads: tumor run, normal run */
+    if (!(diag & 1u)) packed_bitonic_flip<M, K>(v);
     uint16_t *rec = reinterpret_cast<uint16_t *>(stage);
 #pragma unroll
-    for (int r = 0; r < K; ++r) {
+    for (int m = 0; m < M; ++m) {
+        const uint32_t nt = S[m].nt, nn = S[m].nn, bt = S[m].bt, bn = S[m].bn;
+        /* group boundaries (sample, base) */
+        uint32_t c1, c2, c3, c4, c5, c6, c7, c8;
+        if (diag & 32u) {
+            c1 = 0; c2 = 0; c3 = 0; c4 = nt; c5 = nt; c6 = nt; c7 = nt; c8 = nt + nn;
+        } else {
+            c1 = count_below<K>(v[m], 1u << 13); c2 = count_below<K>(v[m], 2u << 13);
+            c3 = count_below<K>(v[m], 3u << 13); c4 = count_below<K>(v[m], 4u << 13);
+            c5 = count_below<K>(v[m], 5u << 13); c6 = count_below<K>(v[m], 6u << 13);
+            c7 = count_below<K>(v[m], 7u << 13); c8 = count_below<K>(v[m], 0xffffu);
+        }
+        /* fold records back over the staged reads: tumor run, normal run */
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
-            const uint32_t key = (v[r] >> (16 * h)) & 0xffffu;
-            if (e < c8) {
-                const uint32_t idx = e < c4 ? 2u * bt + e : 2u * bn + (e - c4);
-                rec[idx] = (uint16_t)key_to_rec(key);
+        for (int r = 0; r < K; ++r) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
+                const uint32_t key = (v[m][r] >> (16 * h)) & 0xffffu;
+                if (e < c8 && !(diag & 64u)) {
+                    const uint32_t idx = e < c4 ? 2u * bt + e : 2u * bn + (e - c4);
+                    rec[idx] = (uint16_t)key_to_rec(key);
+                }
             }
         }
-    }
-    const uint32_t rms_t = wave_sum(rs_t), rms_n = wave_sum(rs_n);
-    if (lane == 0) {
-        st_t.rec_n = 2u * bt | nt << 16;
-        st_t.cnt01 = c1 | (c2 - c1) << 16;
-        st_t.cnt23 = (c3 - c2) | (c4 - c3) << 16;
-        st_t.rms = rms_t;
-        st_n.rec_n = 2u * bn | nn << 16;
-        st_n.cnt01 = (c5 - c4) | (c6 - c5) << 16;
-        st_n.cnt23 = (c7 - c6) | (c8 - c7) << 16;
-        st_n.rms = rms_n;
+        const uint32_t rms_t = (diag & 128u) ? rs_t[m] : wave_sum(rs_t[m]);
+        const uint32_t rms_n = (diag & 128u) ? rs_n[m] : wave_sum(rs_n[m]);
+        if (lane == 0) {
+            Slot3 &st_t = slot[2 * m], &st_n = slot[2 * m + 1];
+            st_t.rec_n = 2u * bt | nt << 16;
+            st_t.cnt01 = c1 | (c2 - c1) << 16;
+            st_t.cnt23 = (c3 - c2) | (c4 - c3) << 16;
+            st_t.rms = rms_t;
+            st_n.rec_n = 2u * bn | nn << 16;
+            st_n.cnt01 = (c5 - c4) | (c6 - c5) << 16;
+            st_n.cnt23 = (c7 - c6) | (c8 - c7) << 16;
+            st_n.rms = rms_n;
+        }
     }
 }
 
-/* one ordered fold step (sniper_maqcns.c:165-172) on a record */
-__device__ __forceinline__ void fold_step(uint32_t rc, const double *fk, float &es, float &fs,
-                                          uint32_t &w0, uint32_t &w1)
-{
-    const uint32_t q = rc & 0xffu, st = rc >> 8;
-    const uint32_t w = st ? w1 : w0;
-    const double f = fk[w];
-    es = (float)((double)es + f * (double)q);
-    fs = (float)((double)fs + f);
-    const uint32_t wn = w < 255u ? w + 1u : 255u;
-    if (st) w1 = wn; else w0 = wn;
-}
-
-/* Fold of one (site, sample): its four base groups, the longest first. */
+/* Fold of one (site, sample) by TWO lanes: role 0 accumulates esum, role 1
+ * fsum (sniper_maqcns.c:165-172).  Both run the same instruction stream:
+ *   acc = (float)((double)acc + fk[w] * m),  m = q (esum) or 1.0 (fsum),
+ * and fk[w]*1.0 == fk[w] exactly, so each chain is bit-identical to the
+ * reference's while the wave issues 5 f64 operations per step instead of 8.
+ * Base groups are walked longest first, so the wave-wide trip count is set by
+ * one long chain per lane. */
 __device__ __forceinline__ void fold_sample(const uint16_t *rec, const uint32_t cnt[4],
-                                            const double *fk, float es[4], float fs[4])
+                                            const double *fk, uint32_t role, float acc[4])
 {
-    uint32_t start[4], order[4];
-    start[0] = 0;
-    start[1] = cnt[0];
-    start[2] = cnt[0] + cnt[1];
-    start[3] = start[2] + cnt[2];
-    /* longest group first, the rest in base order */
+    const uint32_t start1 = cnt[0], start2 = cnt[0] + cnt[1], start3 = start2 + cnt[2];
     uint32_t L = 0;
 #pragma unroll
-    for (int b = 1; b < 4; ++b) L = cnt[b] > cnt[L] ? (uint32_t)b : L;
-    order[0] = L;
-    {
-        int o = 1;
+    for (uint32_t b = 1; b < 4; ++b) L = cnt[b] > (L == 0 ? cnt[0] : (L == 1 ? cnt[1] : cnt[2])) ? b : L;
 #pragma unroll
-        for (uint32_t b = 0; b < 4; ++b)
-            if (b != L) order[o++] = b;
-    }
+    for (int b = 0; b < 4; ++b) acc[b] = 0.0f;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) { es[b] = 0.0f; fs[b] = 0.0f; }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t b = order[i];
-        const uint32_t s0 = b == 0 ? start[0] : (b == 1 ? start[1] : (b == 2 ? start[2] : start[3]));
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t b = i == 0 ? L : (i - 1u) + ((i - 1u) >= L ? 1u : 0u);
+        const uint32_t s0 = b == 0 ? 0u : (b == 1 ? start1 : (b == 2 ? start2 : start3));
         uint32_t t = b == 0 ? cnt[0] : (b == 1 ? cnt[1] : (b == 2 ? cnt[2] : cnt[3]));
-        float e = 0.0f, f = 0.0f;
+        float e = 0.0f;
         uint32_t w0 = 0, w1 = 0;
         uint32_t nxt = t ? rec[s0 + t - 1] : 0u;
         while (t) {
             --t;
             const uint32_t cur = nxt;
             if (t) nxt = rec[s0 + t - 1];
-            fold_step(cur, fk, e, f, w0, w1);
+            const uint32_t st = cur >> 8;
+            const uint32_t w = st ? w1 : w0;
+            const double f = fk[w];
+            const uint32_t mul = role ? 1u : (cur & 0xffu);
+            e = (float)((double)e + f * (double)mul);
+            const uint32_t wn = w < 255u ? w + 1u : 255u;
+            if (st) w1 = wn; else w0 = wn;
         }
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; ++bb)
-            if (bb == b) { es[bb] = e; fs[bb] = f; }
+            if (bb == b) acc[bb] = e;
     }
 }
 
@@ -1102,19 +1124,26 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
                                            bool have_next, const Sub &nxt)
 {
     const uint32_t lane = lane_id();
-    const int sl = (int)lane;                      /* slot = site * 2 + sample */
-    float es[4], fs[4];
-    uint32_t cnt[4];
-    if (sl < 2 * G) {
+    const int sl = (int)(lane >> 1);               /* slot = site * 2 + sample */
+    const uint32_t role = lane & 1u;               /* 0: esum lane, 1: fsum lane */
+    const bool act = sl < 2 * G;
+    float acc[4];
+    uint32_t cnt[4], depth = 0, rms = 0;
+    if (act) {
         const Slot3 &m3 = slot[sl];
         cnt[0] = m3.cnt01 & 0xffffu; cnt[1] = m3.cnt01 >> 16;
         cnt[2] = m3.cnt23 & 0xffffu; cnt[3] = m3.cnt23 >> 16;
+        depth = m3.rec_n >> 16;
+        rms = m3.rms;
         const uint16_t *rec = reinterpret_cast<const uint16_t *>(stage) + (m3.rec_n & 0xffffu);
-        if (!(a.diag & 2u)) fold_sample(rec, cnt, fk, es, fs);
+        if (!(a.diag & 2u)) fold_sample(rec, cnt, fk, role, acc);
         else {
 #pragma unroll
-            for (int b = 0; b < 4; ++b) { es[b] = (float)cnt[b]; fs[b] = es[b]; }
+            for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b];
         }
+    } else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
     }
     /* every fold record has been read: the next sub-group's reads may now
      * stream into the stage while the likelihoods are computed */
@@ -1123,11 +1152,34 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         issue_dma(a, nxt, stage);
     }
-    if (sl < 2 * G) {
-        const Slot3 &m3 = slot[sl];
+    /* exchange esum / fsum within the lane pair (DPP, all lanes active) */
+    float es[4], fs[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const float o = __builtin_bit_cast(float, xor_lane<1>(__builtin_bit_cast(uint32_t, acc[b])));
+        es[b] = role ? o : acc[b];
+        fs[b] = role ? acc[b] : o;
+    }
+    /* likelihoods: role 0 evaluates genotypes 0..4, role 1 genotypes 5..9 */
+    uint32_t c[4];
+    const uint32_t tot = rescale_counts(cnt, c);
+    float mine[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        int j, k;
+        geno_jk((int)role * 5 + t, j, k);
+        mine[t] = (act && !(a.diag & 4u)) ? geno_p(j, k, es, fs, c, tot, a.m) : 0.0f;
+    }
+    float p[10];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        const float o = __builtin_bit_cast(float, xor_lane<1>(__builtin_bit_cast(uint32_t, mine[t])));
+        p[t] = role ? o : mine[t];
+        p[5 + t] = role ? mine[t] : o;
+    }
+    if (act && role == 0u) {
         uint32_t lk[10], min_lk, rms_q, cns;
-        const uint32_t depth = m3.rec_n >> 16;
-        if (!(a.diag & 4u)) glf_and_cns_lane(es, fs, cnt, depth, m3.rms, a.m, lk, min_lk, rms_q, cns);
+        if (!(a.diag & 4u)) glf_finish(p, es, depth, rms, a.m, lk, min_lk, rms_q, cns);
         else {
 #pragma unroll
             for (int g = 0; g < 10; ++g) lk[g] = (uint32_t)es[g & 3] & 0xffu;
@@ -1142,7 +1194,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
         if (a.glf) {
             const uint32_t s = (uint32_t)sl >> 1;
             store_glf(&a.glf[2ull * sites[s] + (sl & 1)], a.m.nt16[refcs[s] & 0xffu], lk, min_lk,
-                      rms_q, r.depth);
+                      rms_q, depth);
         }
     }
     wave_sync();
@@ -1203,19 +1255,37 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the sub-group's reads are in LDS */
         /* ---- phase A ---- */
         int G = 0;
-        for (uint32_t i = cur.a; i < cur.b; ++i) {
-            const uint32_t site = (uint32_t)(blk * GB + i);
-            const uint32_t t_i = D_T(i), nt = D_T(i + 1u) - t_i;
-            const uint32_t n_i = D_N(i), nn = D_N(i + 1u) - n_i;
-            const uint32_t rdesc = D_REF(i);
-            const uint32_t refc = rdesc & 0xffu, ref16 = rdesc >> 8;
-            const uint32_t bt = t_i - cur.t0, bn = cur.lt + (n_i - cur.n0);
-            if (lane == 0) { sites[G] = site; refcs[G] = refc; }
-            const uint32_t tot = nt + nn;
-            if (tot <= 128u) sort_site<1>(stage, bt, nt, bn, nn, ref16, cap, slot[2 * G], slot[2 * G + 1], a.diag);
-            else if (tot <= 256u) sort_site<2>(stage, bt, nt, bn, nn, ref16, cap, slot[2 * G], slot[2 * G + 1], a.diag);
-            else sort_site<4>(stage, bt, nt, bn, nn, ref16, cap, slot[2 * G], slot[2 * G + 1], a.diag);
+        for (uint32_t i = cur.a; i < cur.b;) {
+            SiteA S2[2];
+            uint32_t tot[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const uint32_t j = i + (uint32_t)m < cur.b ? i + (uint32_t)m : i;
+                const uint32_t t_i = D_T(j), n_i = D_N(j);
+                const uint32_t rdesc = D_REF(j);
+                S2[m].nt = D_T(j + 1u) - t_i;
+                S2[m].nn = D_N(j + 1u) - n_i;
+                S2[m].bt = t_i - cur.t0;
+                S2[m].bn = cur.lt + (n_i - cur.n0);
+                S2[m].ref16 = rdesc >> 8;
+                tot[m] = S2[m].nt + S2[m].nn;
+                if (lane == 0 && i + (uint32_t)m < cur.b) {
+                    sites[G + m] = (uint32_t)(blk * GB + j);
+                    refcs[G + m] = rdesc & 0xffu;
+                }
+            }
+            if (i + 1u < cur.b && tot[0] <= 128u && tot[1] <= 128u) {
+                sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, a.diag);   /* two sites, interleaved */
+                G += 2;
+                i += 2;
+                continue;
+            }
+            SiteA S1[1] = {S2[0]};
+            if (tot[0] <= 128u) sort_sites<1, 1>(stage, S1, cap, slot + 2 * G, a.diag);
+            else if (tot[0] <= 256u) sort_sites<2, 1>(stage, S1, cap, slot + 2 * G, a.diag);
+            else sort_sites<4, 1>(stage, S1, cap, slot + 2 * G, a.diag);
             ++G;
+            ++i;
         }
         wave_sync();
         /* ---- next sub-group: same block, else the next non-empty block ---- */
