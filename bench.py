@@ -147,15 +147,9 @@ def main():
     elapsed = t1 - t0
     kms = ctx.kernel_time_log()
     sites_rank = S * args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        s = torch.tensor([sites_rank], dtype=torch.float64, device=dev)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        total_sites = float(s.item())
-    else:
-        total_sites = float(sites_rank)
+    import importlib
+    sharding = importlib.import_module("somatic_sniper_amd.sharding")
+    elapsed, total_sites, _ = sharding.aggregate(elapsed, sites_rank, world)
 
     avg_kernel_ms = float(np.mean(kms)) if len(kms) else None
     alg_bytes = float(np.mean([bytes_per_batch[k] for k in used]))
