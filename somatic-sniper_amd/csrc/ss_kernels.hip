@@ -7,22 +7,19 @@
  * calls (sniper_glf2cns, :250-273) and the Phred-space somatic posterior.
  *
  * Work decomposition (DESIGN.md "Kernels"):
- *   ss_score_main   one 64-lane wave scores a GROUP of up to 8 sites:
- *     A  per site and sample, the wave loads the packed reads (coalesced),
- *        builds order keys and bitonic-sorts them in registers (1/2/4 keys per
- *        lane); sorted keys land in a per-wave LDS arena, grouped by base.
- *     B  ordered fold: lane (site, sample, base) walks its base group in
- *        descending key order accumulating esum/fsum -- the reference's float
- *        accumulators fed double increments (sniper_maqcns.c:162-172); this is
- *        the inherently serial part, 64 independent chains per wave.
- *     C  every lane evaluates the 10 genotype likelihoods + quantisation +
- *        consensus for its (site, sample) from quad-shuffled sums.
- *     D  lane s decides site s: gate, SNV candidate test, posteriors, joint
- *        prior, emit filter; emitted sites are compacted with one atomic.
- *   ss_score_deep   one 256-thread block per site with a sample deeper than
- *        SS_MAIN_MAXN: block bitonic sort in LDS (<= SS_DEEP_MAXN keys per
- *        sample) or, for giant pileups, in a global scratch slice; then the
- *        same B/C/D device code.
+ *   ss_score_main   persistent waves walk 16-site blocks.  A block's reads are
+ *     staged into LDS by LDS-DMA; per site ONE wave-wide bitonic sort of 16-bit
+ *     keys (two per VGPR, both samples) orders the reads, which become 16-bit
+ *     fold records written back over the staged reads.  Then two lanes per
+ *     (site, sample) run the ordered esum / fsum fold (the reference's float
+ *     accumulators fed double increments, sniper_maqcns.c:162-172), split the
+ *     10 genotype likelihoods between them, and lane s decides site s (gate,
+ *     SNV candidate test, posteriors / joint prior, emit filter).  The DMA of
+ *     the next sub-group overlaps the likelihood and decision phases.
+ *   ss_score_deep   one 256-thread block per site with more than PK_MAX reads:
+ *     block bitonic sort of 32-bit keys in LDS (<= SS_DEEP_MAXN per sample) or,
+ *     for giant pileups, in a global scratch slice; then the same fold,
+ *     likelihood and decision code (quad-cooperative variant).
  *
  * Bit-exactness: built with -ffp-contract=off (no FMA contraction); float
  * division and double sqrt are correctly rounded (sqrt re-checked with fma);
@@ -93,46 +90,6 @@ __device__ __forceinline__ uint32_t read_key(uint32_t rd, uint32_t ref16, uint32
     return valid ? (base << 26 | minq << 18 | hb << 17 | st << 16 | bq << 8 | mq) : SENT;
 }
 
-/* --------------------------------------------------------------------------
- * Wave bitonic sort, ascending, of 64*K keys held lane-major (element
- * e = lane*K + r in v[r]).  Distances < K are register compare-exchanges,
- * larger ones cross lanes.  Input placement is arbitrary.
- * ------------------------------------------------------------------------ */
-template <int K>
-__device__ __forceinline__ void wave_bitonic(uint32_t (&v)[K])
-{
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (uint32_t k = 2; k <= 64u * K; k <<= 1) {
-#pragma unroll
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            if (j >= (uint32_t)K) {
-                const int lj = (int)(j / K);
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    const uint32_t e = lane * K + r;
-                    const uint32_t o = (uint32_t)__shfl_xor((int)v[r], lj);
-                    const bool up = (e & k) == 0u, lower = (e & j) == 0u;
-                    v[r] = (lower == up) ? (v[r] < o ? v[r] : o) : (v[r] > o ? v[r] : o);
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    const int r2 = r ^ (int)j;
-                    if (r2 > r) {
-                        const uint32_t e = lane * K + r;
-                        const bool up = (e & k) == 0u;
-                        const uint32_t a = v[r], b = v[r2];
-                        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-                        v[r] = up ? lo : hi;
-                        v[r2] = up ? hi : lo;
-                    }
-                }
-            }
-        }
-    }
-}
-
 /* per (site, sample) bookkeeping kept in LDS */
 struct SlotMeta {
     uint32_t base;      /* arena offset of the sorted keys */
@@ -153,48 +110,6 @@ struct SiteInfo {
     uint32_t site;
     uint32_t refc;
 };
-
-/* Phase A for one sample of one site, K keys per lane (n <= 64*K). */
-template <int K>
-__device__ __forceinline__ void sort_sample(const uint32_t *__restrict__ reads, uint32_t n,
-                                            uint32_t ref16, uint32_t cap, uint32_t *arena,
-                                            SlotMeta &meta, uint32_t &nvalid, uint32_t diag)
-{
-    const uint32_t lane = lane_id();
-    uint32_t v[K];
-    uint32_t rs = 0;
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-        const uint32_t idx = (uint32_t)r * 64u + lane;   /* coalesced load */
-        uint32_t t = 0;
-        v[r] = SENT;
-        if (idx < n) {
-            v[r] = read_key(reads[idx], ref16, cap, t);
-            rs += t;
-        }
-    }
-    if (!(diag & 1u)) wave_bitonic<K>(v);
-    uint32_t nv = 0, c1 = 0, c2 = 0, c3 = 0;
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-        nv += (uint32_t)__popcll(__ballot(v[r] != SENT));
-        c1 += (uint32_t)__popcll(__ballot(v[r] < (1u << 26)));
-        c2 += (uint32_t)__popcll(__ballot(v[r] < (2u << 26)));
-        c3 += (uint32_t)__popcll(__ballot(v[r] < (3u << 26)));
-    }
-#pragma unroll
-    for (int r = 0; r < K; ++r)
-        if (v[r] != SENT) arena[lane * K + r] = v[r];
-    const uint32_t rms = wave_sum(rs);
-    if (lane == 0) {
-        meta.start[0] = 0; meta.start[1] = c1; meta.start[2] = c2; meta.start[3] = c3;
-        meta.cnt[0] = c1; meta.cnt[1] = c2 - c1; meta.cnt[2] = c3 - c2; meta.cnt[3] = nv - c3;
-        meta.n = n;
-        meta.rms_lo = rms;
-        meta.rms_hi = 0;
-    }
-    nvalid = nv;
-}
 
 /* --------------------------------------------------------------------------
  * Phase B: ordered fold of one base group (sniper_maqcns.c:162-172).
@@ -403,24 +318,6 @@ __device__ __forceinline__ void glf_and_cns(int q, const float es[4], const floa
     glf_finish(p, es, n, rms, m, lk, min_lk, rms_q, cns);
 }
 
-/* single-lane version (main kernel: one lane per (site, sample)) */
-__device__ __forceinline__ void glf_and_cns_lane(const float es[4], const float fs[4],
-                                                 const uint32_t craw[4], uint32_t n, uint64_t rms,
-                                                 const ss_dev_model &m, uint32_t lk[10],
-                                                 uint32_t &min_lk, uint32_t &rms_q, uint32_t &cns)
-{
-    uint32_t c[4];
-    const uint32_t tot = rescale_counts(craw, c);
-    float p[10];
-#pragma unroll
-    for (int g = 0; g < 10; ++g) {
-        int j, k;
-        geno_jk(g, j, k);
-        p[g] = geno_p(j, k, es, fs, c, tot, m);
-    }
-    glf_finish(p, es, n, rms, m, lk, min_lk, rms_q, cns);
-}
-
 /* qAdd (somatic_sniper.c:18) with the out-of-range index clamped + counted */
 __device__ __forceinline__ int qadd(const int32_t *T, int x, int y, int &clamped)
 {
@@ -478,9 +375,12 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
             if (j != bj) jcq = qadd(m.qadd, jcq, l, clamped);  /* stale-index quirk, :196 */
         }
         if (jcq > 255) jcq = 255;
-        const int gb[10] = {1, 3, 5, 9, 2, 6, 10, 4, 12, 8};
-        jn = gb[bi];
-        jt = gb[bj];
+        /* glfBase (somatic_sniper.c:26): genotype index -> nt16 bit set */
+        int gj, gk;
+        geno_jk(bi, gj, gk);
+        jn = 1 << gj | 1 << gk;
+        geno_jk(bj, gj, gk);
+        jt = 1 << gj | 1 << gk;
     } else {
         /* calculatePosteriors (:79-99) for both samples, then the sum (:209-214);
          * x_j is recomputed in the second pass instead of kept in an array */
@@ -640,16 +540,11 @@ struct Slot3 {
     uint32_t rms;        /* sum of min(mapQ & 0x7f, cap)^2 */
 };
 
-struct Res3 {
-    uint32_t lk[3];      /* 10 bytes packed */
-    uint32_t cns;
-    uint32_t depth;
-};
 
 struct MainLds {
     uint32_t stage[4][STG];
     Slot3    slot[4][2 * GB];
-    Res3     res[4][2 * GB];
+    SlotRes  res[4][2 * GB];
     uint32_t site[4][GB];
     uint32_t refc[4][GB];
 };
@@ -726,65 +621,6 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
     } else {
         static_assert(LJ == 63, "unsupported lane xor");
         return xor_lane<32>(xor_lane<31>(x));
-    }
-}
-
-__device__ __forceinline__ uint32_t xor_lane_dyn(uint32_t x, int lj)
-{
-    switch (lj) {
-    case 1: return xor_lane<1>(x);
-    case 2: return xor_lane<2>(x);
-    case 4: return xor_lane<4>(x);
-    case 8: return xor_lane<8>(x);
-    case 16: return xor_lane<16>(x);
-    default: return xor_lane<32>(x);
-    }
-}
-
-/* Bitonic sort, ascending, of 128*K u16 keys: element e = lane*2K + 2r + h
- * lives in half h of v[r]. */
-template <int K>
-__device__ __forceinline__ void packed_bitonic(uint32_t (&v)[K])
-{
-    const uint32_t lane = lane_id();
-    constexpr uint32_t E = 2u * K;          /* elements per lane */
-#pragma unroll
-    for (uint32_t k = 2; k <= 128u * K; k <<= 1) {
-#pragma unroll
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            if (j >= E) {                   /* across lanes */
-                const int lj = (int)(j / E);
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    const uint32_t e = lane * E + 2u * r;
-                    const uint32_t o = xor_lane_dyn(v[r], lj);   /* lj is a constant after unrolling */
-                    const bool up = (e & k) == 0u, lower = (e & j) == 0u;
-                    const uint32_t mn = pk_min(v[r], o), mx = pk_max(v[r], o);
-                    v[r] = (lower == up) ? mn : mx;
-                }
-            } else if (j >= 2u) {           /* across registers of a lane */
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    const int r2 = r ^ (int)(j >> 1);
-                    if (r2 > r) {
-                        const uint32_t e = lane * E + 2u * r;
-                        const bool up = (e & k) == 0u;
-                        const uint32_t mn = pk_min(v[r], v[r2]), mx = pk_max(v[r], v[r2]);
-                        v[r] = up ? mn : mx;
-                        v[r2] = up ? mx : mn;
-                    }
-                }
-            } else {                        /* the two halves of a register */
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    const uint32_t e = lane * E + 2u * r;
-                    const bool up = (e & k) == 0u;
-                    const uint32_t sw = (v[r] >> 16) | (v[r] << 16);
-                    const uint32_t mn = pk_min(v[r], sw), mx = pk_max(v[r], sw);
-                    v[r] = up ? ((mn & 0xffffu) | (mx & 0xffff0000u)) : ((mx & 0xffffu) | (mn & 0xffff0000u));
-                }
-            }
-        }
     }
 }
 
@@ -1119,7 +955,7 @@ __device__ __forceinline__ void issue_dma(const ss_score_args &a, const Sub &r, 
 
 /* Phases B, C, D for the G sites of a sub-group. */
 __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32_t *stage,
-                                           const Slot3 *slot, Res3 *res, const uint32_t *sites,
+                                           const Slot3 *slot, SlotRes *res, const uint32_t *sites,
                                            const uint32_t *refcs, const double *fk,
                                            bool have_next, const Sub &nxt)
 {
@@ -1185,10 +1021,11 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
             for (int g = 0; g < 10; ++g) lk[g] = (uint32_t)es[g & 3] & 0xffu;
             min_lk = 0; rms_q = 0; cns = (uint32_t)fs[0];
         }
-        Res3 &r = res[sl];
-        r.lk[0] = lk[0] | lk[1] << 8 | lk[2] << 16 | lk[3] << 24;
-        r.lk[1] = lk[4] | lk[5] << 8 | lk[6] << 16 | lk[7] << 24;
-        r.lk[2] = lk[8] | lk[9] << 8;
+        SlotRes &r = res[sl];
+        uint32_t *rw = reinterpret_cast<uint32_t *>(r.lk);
+        rw[0] = lk[0] | lk[1] << 8 | lk[2] << 16 | lk[3] << 24;
+        rw[1] = lk[4] | lk[5] << 8 | lk[6] << 16 | lk[7] << 24;
+        rw[2] = lk[8] | lk[9] << 8;
         r.cns = cns;
         r.depth = depth;
         if (a.glf) {
@@ -1199,17 +1036,9 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
     }
     wave_sync();
     if ((int)lane < G) {
-        const Res3 &rt = res[2 * lane], &rn = res[2 * lane + 1];
-        SlotRes t, n;
-#pragma unroll
-        for (int g = 0; g < 10; ++g) {
-            t.lk[g] = (uint8_t)(rt.lk[g >> 2] >> (8 * (g & 3)));
-            n.lk[g] = (uint8_t)(rn.lk[g >> 2] >> (8 * (g & 3)));
-        }
-        t.cns = rt.cns; t.depth = rt.depth;
-        n.cns = rn.cns; n.depth = rn.depth;
-        if (!(a.diag & 8u)) decide_site(a, sites[lane], refcs[lane], t, n);
-        else a.score[sites[lane]] = (int32_t)rt.cns;
+        /* the decision reads both samples' records straight from LDS */
+        if (!(a.diag & 8u)) decide_site(a, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
+        else a.score[sites[lane]] = (int32_t)res[2 * lane].cns;
     }
     wave_sync();
 }
@@ -1227,7 +1056,7 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
 
     uint32_t *stage = L.stage[wv];
     Slot3 *slot = L.slot[wv];
-    Res3 *res = L.res[wv];
+    SlotRes *res = L.res[wv];
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
     const uint64_t nwaves = (uint64_t)gridDim.x * (SS_MAIN_BLOCK / 64);
     const uint64_t nblocks = (a.n_sites + GB - 1) / GB;

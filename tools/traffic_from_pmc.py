@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""profiles/traffic.json from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE)
+of `bench.py --no-cpu` (tools/profile_round.sh).  gfx950 correction per
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports half of the streamed read
+bytes, so it is doubled; both counters are in KiB.  Per-launch mean over the
+ss_score_main dispatches.
+
+    python tools/traffic_from_pmc.py gpurun_out/r01c [--sites N --lt 60 --ln 30]
+"""
+import argparse
+import csv
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_launch(path, counter, kernel):
+    vals = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == counter and r["Kernel_Name"].startswith(kernel + "("):
+                vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    assert vals, f"no {counter} rows for {kernel} in {path}"
+    return sum(vals.values()) / len(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run_dir")
+    ap.add_argument("--kernel", default="ss_score_main")
+    ap.add_argument("--sites", type=int, default=1 << 24)
+    ap.add_argument("--lt", type=float, default=60.0)
+    ap.add_argument("--ln", type=float, default=30.0)
+    ap.add_argument("--algorithmic-bytes", type=float, default=None,
+                    help="per launch; default: from the bench.json in run_dir")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    a = ap.parse_args()
+    fk, nf = per_launch(os.path.join(a.run_dir, "pmc_FETCH_SIZE", "run_counter_collection.csv"),
+                        "FETCH_SIZE", a.kernel)
+    wk, nw = per_launch(os.path.join(a.run_dir, "pmc_WRITE_SIZE", "run_counter_collection.csv"),
+                        "WRITE_SIZE", a.kernel)
+    alg = a.algorithmic_bytes
+    if alg is None:
+        b = json.loads(open(os.path.join(a.run_dir, "bench.json")).read().strip().splitlines()[-1])
+        alg = b["roofline"]["algorithmic_bytes_per_launch"]
+    rd, wr = 2.0 * fk * 1024.0, wk * 1024.0
+    out = {"kernel": a.kernel, "sites": a.sites, "lt": a.lt, "ln": a.ln,
+           "fetch_size_kb_raw": fk, "write_size_kb_raw": wk, "launches": [nf, nw],
+           "correction": "FETCH_SIZE doubled (gfx950 reports 1/2 of streamed read bytes, "
+                         "MI355X_MICROARCH.md HBM section); units KiB",
+           "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+           "hbm_bytes_per_launch": rd + wr, "algorithmic_bytes_per_launch": alg,
+           "traffic_over_algorithmic": (rd + wr) / alg,
+           "source": f"{a.run_dir}/pmc_*/run_counter_collection.csv (rocprofv3 --pmc FETCH_SIZE / "
+                     "WRITE_SIZE, separate passes, bench.py --steps 3 --warmup 1 --no-cpu)"}
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
