@@ -108,6 +108,8 @@ static void shim_init(pu_data2_t *d)
     c = 0; g_b.off_t = grow(NULL, &c, g_b.cap + 1, 4);
     c = 0; g_b.off_n = grow(NULL, &c, g_b.cap + 1, 4);
     g_b.off_t[0] = g_b.off_n[0] = 0;
+    g_b.calls_cap = 0;   /* emitted calls are only collected into a non-empty buffer */
+    g_b.calls = grow(NULL, &g_b.calls_cap, 4096, sizeof(ss_call_t));
     g_d = d;
 }
 
