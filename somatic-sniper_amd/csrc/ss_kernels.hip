@@ -534,7 +534,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void glb_void_t;
 
 struct Slot3 {
-    uint32_t rec_n;      /* u16 index of the fold records | non-deleted depth << 16 */
+    uint32_t rec_n;      /* u32 index of the fold records | non-deleted depth << 16 */
     uint32_t cnt01;      /* cnt[0] | cnt[1] << 16 */
     uint32_t cnt23;      /* cnt[2] | cnt[3] << 16 */
     uint32_t rms;        /* sum of min(mapQ & 0x7f, cap)^2 */
@@ -549,28 +549,51 @@ struct MainLds {
     uint32_t refc[4][GB];
 };
 
-/* 16-bit order key (see the section comment); 0xffff = no contribution. */
-__device__ __forceinline__ uint32_t read_key16(uint32_t rd, uint32_t ref16, uint32_t sample)
+/* 16-bit order key (see the section comment); 0xffff = no contribution.
+ *   sample<<15 | base<<13 | minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz
+ * E = baseQ >> 6 and nz = (baseQ & 0x3f) != 0 order the reads of one
+ * (minq < 4, hasbase, strand) class exactly as the reference's baseQ tie-break
+ * does as far as the clamp of sniper_maqcns.c:165 is concerned (classes
+ * 1..63 | 64 | 65..127 | 128 | ...); for minq >= 4 they only reorder reads with
+ * identical (q, strand), which leaves every sum unchanged.
+ * base / hasbase come from two per-site tables with 2-bit fields indexed by
+ * 2*nt16 (entry 0, '=', already resolved to the reference base):
+ * tb = base, th = hasbase; see nt_tables(). */
+__device__ __forceinline__ uint32_t read_key16(uint32_t rd, uint32_t tb, uint32_t th,
+                                               uint32_t samplebit)
 {
-    const uint32_t mq = rd & 0xffu, bq = (rd >> 8) & 0xffu;
-    const uint32_t nt = (rd >> 16) & 0xfu, st = (rd >> 20) & 1u;
-    const uint32_t minq = mq < bq ? mq : bq;
-    const bool valid = minq != 0u || (bq & 0x3fu) != 0u;
-    const uint32_t nt4 = nt16_to_nt4(nt ? nt : ref16);
-    const uint32_t hb = nt4 < 4u ? 1u : 0u;
-    const uint32_t base = hb ? nt4 : 0u;
-    uint32_t t = 0;
-    if (minq < 4u)
-        t = (bq >= 64u) + (bq > 64u) + (bq >= 128u) + (bq > 128u) + (bq >= 192u) + (bq > 192u);
-    return valid ? (sample << 15 | base << 13 | minq << 5 | hb << 4 | st << 3 | t) : 0xffffu;
+    const uint32_t minq = min(rd & 0xffu, (rd >> 8) & 0xffu);
+    const uint32_t lo6 = rd & 0x3f00u;
+    const uint32_t nz = lo6 != 0u ? 1u : 0u;
+    const uint32_t nt2 = (rd >> 15) & 0x1eu;
+    const uint32_t base = __builtin_amdgcn_ubfe(tb, nt2, 2u);
+    const uint32_t hb = __builtin_amdgcn_ubfe(th, nt2, 1u);
+    const uint32_t E = __builtin_amdgcn_ubfe(rd, 14u, 2u);
+    const uint32_t st = __builtin_amdgcn_ubfe(rd, 20u, 1u);
+    const uint32_t key = samplebit | base << 13 | minq << 5 | hb << 4 | st << 3 | E << 1 | nz;
+    return (minq | lo6) != 0u ? key : 0xffffu;
 }
 
-/* fold record of a sorted key: clamped q (sniper_maqcns.c:165) | strand << 8 */
+/* per-site base tables of read_key16 (bam_nt16_nt4_table semantics,
+ * sniper_maqcns.c:19,153-154: single-base codes -> 0..3 with hasbase, every
+ * other code counts as A without hasbase; code 0 '=' -> the reference base). */
+__device__ __forceinline__ void nt_tables(uint32_t ref16, uint32_t &tb, uint32_t &th)
+{
+    constexpr uint32_t TB = 1u << 4 | 2u << 8 | 3u << 16;     /* C=2 -> 1, G=4 -> 2, T=8 -> 3 */
+    constexpr uint32_t TH = 1u << 2 | 1u << 4 | 1u << 8 | 1u << 16;
+    tb = TB | ((TB >> (2u * ref16)) & 3u);
+    th = TH | ((TH >> (2u * ref16)) & 1u);
+}
+
+/* fold record of a sorted key (u32):
+ *   bits 0..7   clamped q (sniper_maqcns.c:165)   -- esum multiplier
+ *   bit  16     1                                  -- fsum multiplier
+ *   bits 24..31 strand << 4 (the field offset of its w counter, see fold_sample) */
 __device__ __forceinline__ uint32_t key_to_rec(uint32_t k)
 {
-    const uint32_t minq = (k >> 5) & 0xffu, st = (k >> 3) & 1u, weird = k & 1u;
-    const uint32_t q = (minq < 4u && !weird) ? 4u : minq;
-    return q | st << 8;
+    const uint32_t minq = (k >> 5) & 0xffu, st = (k >> 3) & 1u, nz = k & 1u;
+    const uint32_t q = (minq < 4u && nz) ? 4u : minq;
+    return q | 1u << 16 | st << 28;
 }
 
 __device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b)
@@ -761,34 +784,40 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
     const uint32_t lane = lane_id();
     uint32_t v[M][K];
     uint32_t rs_t[M], rs_n[M];
+    /* input placement: tumor reads at elements [0, nt), normal reads at
+     * [ntr, ntr + nn) with ntr = nt rounded up to even, so the two elements of
+     * a lane (e0 = 2*(r*64 + lane), e0 + 1) are adjacent reads of ONE sample
+     * and come from LDS with one ds_read2 (the pad element is invalid). */
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-        rs_t[m] = 0;
-        rs_n[m] = 0;
-        const uint32_t nt = S[m].nt, nn = S[m].nn;
+        const uint32_t nt = S[m].nt, nn = S[m].nn, ntr = nt + (nt & 1u);
+        uint32_t tb, th;
+        nt_tables(S[m].ref16, tb, th);
+        uint32_t a_t = 0, a_n = 0;
 #pragma unroll
         for (int r = 0; r < K; ++r) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t e = ((uint32_t)r * 64u + lane) * 2u + (uint32_t)h;   /* input placement */
-                uint32_t key = 0xffffu;
-                if (e < nt + nn) {
-                    const bool tum = e < nt;
-                    const uint32_t rd = stage[tum ? S[m].bt + e : S[m].bn + (e - nt)];
-                    uint32_t t = rd & 0x7fu;
-                    t = t < cap ? t : cap;
-                    if (tum) rs_t[m] += t * t; else rs_n[m] += t * t;
-                    key = (diag & 16u) ? ((rd & 0x7fffu) | (tum ? 0u : 0x8000u))
-                                       : read_key16(rd, S[m].ref16, tum ? 0u : 1u);
-                }
-                w |= key << (16 * h);
-            }
-            v[m][r] = w;
+            const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
+            const bool tum = e0 < ntr;
+            const uint32_t idx = e0 + (tum ? S[m].bt : S[m].bn - ntr);
+            const uint32_t lim = tum ? nt : ntr + nn;
+            const uint32_t rd0 = stage[idx], rd1 = stage[idx + 1u];
+            const uint32_t sb = tum ? 0u : 0x8000u;
+            uint32_t k0 = (diag & 16u) ? ((rd0 & 0x7fffu) | sb) : read_key16(rd0, tb, th, sb);
+            uint32_t k1 = (diag & 16u) ? ((rd1 & 0x7fffu) | sb) : read_key16(rd1, tb, th, sb);
+            const bool in0 = e0 < lim, in1 = e0 + 1u < lim;
+            k0 = in0 ? k0 : 0xffffu;
+            k1 = in1 ? k1 : 0xffffu;
+            const uint32_t t0 = min(rd0 & 0x7fu, cap), t1 = min(rd1 & 0x7fu, cap);
+            const uint32_t x = (in0 ? t0 * t0 : 0u) + (in1 ? t1 * t1 : 0u);
+            a_t += tum ? x : 0u;
+            a_n += tum ? 0u : x;
+            v[m][r] = k0 | k1 << 16;
         }
+        rs_t[m] = a_t;
+        rs_n[m] = a_n;
     }
     if (!(diag & 1u)) packed_bitonic_flip<M, K>(v);
-    uint16_t *rec = reinterpret_cast<uint16_t *>(stage);
+    uint32_t *rec = stage;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
         const uint32_t nt = S[m].nt, nn = S[m].nn, bt = S[m].bt, bn = S[m].bn;
@@ -810,8 +839,8 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
                 const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
                 const uint32_t key = (v[m][r] >> (16 * h)) & 0xffffu;
                 if (e < c8 && !(diag & 64u)) {
-                    const uint32_t idx = e < c4 ? 2u * bt + e : 2u * bn + (e - c4);
-                    rec[idx] = (uint16_t)key_to_rec(key);
+                    const uint32_t idx = e < c4 ? bt + e : bn + (e - c4);
+                    rec[idx] = key_to_rec(key);
                 }
             }
         }
@@ -819,11 +848,11 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
         const uint32_t rms_n = (diag & 128u) ? rs_n[m] : wave_sum(rs_n[m]);
         if (lane == 0) {
             Slot3 &st_t = slot[2 * m], &st_n = slot[2 * m + 1];
-            st_t.rec_n = 2u * bt | nt << 16;
+            st_t.rec_n = bt | nt << 16;
             st_t.cnt01 = c1 | (c2 - c1) << 16;
             st_t.cnt23 = (c3 - c2) | (c4 - c3) << 16;
             st_t.rms = rms_t;
-            st_n.rec_n = 2u * bn | nn << 16;
+            st_n.rec_n = bn | nn << 16;
             st_n.cnt01 = (c5 - c4) | (c6 - c5) << 16;
             st_n.cnt23 = (c7 - c6) | (c8 - c7) << 16;
             st_n.rms = rms_n;
@@ -835,13 +864,18 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
  * fsum (sniper_maqcns.c:165-172).  Both run the same instruction stream:
  *   acc = (float)((double)acc + fk[w] * m),  m = q (esum) or 1.0 (fsum),
  * and fk[w]*1.0 == fk[w] exactly, so each chain is bit-identical to the
- * reference's while the wave issues 5 f64 operations per step instead of 8.
- * Base groups are walked longest first, so the wave-wide trip count is set by
- * one long chain per lane. */
-__device__ __forceinline__ void fold_sample(const uint16_t *rec, const uint32_t cnt[4],
+ * reference's.  m is pulled out of the record with a lane-dependent bit-field
+ * extract.  The two per-strand w counters live in one register (16-bit
+ * fields, counting in units of 8 = the byte stride of fk), selected by the
+ * record's strand<<4 field and saturated at w = 255 (:170).  Base groups are
+ * walked longest first, so the wave-wide trip count is set by one long chain
+ * per lane. */
+__device__ __forceinline__ void fold_sample(const uint32_t *rec, const uint32_t cnt[4],
                                             const double *fk, uint32_t role, float acc[4])
 {
     const uint32_t start1 = cnt[0], start2 = cnt[0] + cnt[1], start3 = start2 + cnt[2];
+    const uint32_t moff = role ? 16u : 0u, mwid = role ? 1u : 8u;
+    const char *fkb = reinterpret_cast<const char *>(fk);
     uint32_t L = 0;
 #pragma unroll
     for (uint32_t b = 1; b < 4; ++b) L = cnt[b] > (L == 0 ? cnt[0] : (L == 1 ? cnt[1] : cnt[2])) ? b : L;
@@ -851,21 +885,22 @@ __device__ __forceinline__ void fold_sample(const uint16_t *rec, const uint32_t 
     for (uint32_t i = 0; i < 4; ++i) {
         const uint32_t b = i == 0 ? L : (i - 1u) + ((i - 1u) >= L ? 1u : 0u);
         const uint32_t s0 = b == 0 ? 0u : (b == 1 ? start1 : (b == 2 ? start2 : start3));
-        uint32_t t = b == 0 ? cnt[0] : (b == 1 ? cnt[1] : (b == 2 ? cnt[2] : cnt[3]));
+        const uint32_t t = b == 0 ? cnt[0] : (b == 1 ? cnt[1] : (b == 2 ? cnt[2] : cnt[3]));
+        const uint32_t *p0 = rec + s0;
+        const uint32_t *p = p0 + t;
         float e = 0.0f;
-        uint32_t w0 = 0, w1 = 0;
-        uint32_t nxt = t ? rec[s0 + t - 1] : 0u;
-        while (t) {
-            --t;
-            const uint32_t cur = nxt;
-            if (t) nxt = rec[s0 + t - 1];
-            const uint32_t st = cur >> 8;
-            const uint32_t w = st ? w1 : w0;
-            const double f = fk[w];
-            const uint32_t mul = role ? 1u : (cur & 0xffu);
-            e = (float)((double)e + f * (double)mul);
-            const uint32_t wn = w < 255u ? w + 1u : 255u;
-            if (st) w1 = wn; else w0 = wn;
+        uint32_t W = 0;
+#pragma unroll 2
+        while (p != p0) {
+            --p;
+            const uint32_t r = *p;
+            const uint32_t sh = r >> 24;                 /* 0 or 16 */
+            uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
+            w8 = w8 < 2040u ? w8 : 2040u;
+            W += 8u << sh;
+            const double f = *reinterpret_cast<const double *>(fkb + w8);
+            const uint32_t m = __builtin_amdgcn_ubfe(r, moff, mwid);
+            e = (float)((double)e + f * (double)m);
         }
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; ++bb)
@@ -921,8 +956,9 @@ __device__ __forceinline__ Sub form_sub(const ss_score_args &a, uint32_t desc, u
 {
     uint32_t i = pos, tot = 0;
     while (i < nsite) {
-        const uint32_t sz = (D_T(i + 1u) - D_T(i)) + (D_N(i + 1u) - D_N(i));
-        if (sz > PK_MAX) {
+        const uint32_t ntl = D_T(i + 1u) - D_T(i);
+        const uint32_t sz = ntl + (D_N(i + 1u) - D_N(i));
+        if (sz + (ntl & 1u) > PK_MAX) {        /* sort slots incl. the pad element */
             if (i == pos) { push_deep(a, (uint32_t)(sblk + i)); pos = ++i; continue; }
             break;
         }
@@ -957,7 +993,7 @@ __device__ __forceinline__ void issue_dma(const ss_score_args &a, const Sub &r, 
 __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32_t *stage,
                                            const Slot3 *slot, SlotRes *res, const uint32_t *sites,
                                            const uint32_t *refcs, const double *fk,
-                                           bool have_next, const Sub &nxt)
+                                           bool have_next, const Sub &nxt, uint32_t diag)
 {
     const uint32_t lane = lane_id();
     const int sl = (int)(lane >> 1);               /* slot = site * 2 + sample */
@@ -971,8 +1007,8 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
         cnt[2] = m3.cnt23 & 0xffffu; cnt[3] = m3.cnt23 >> 16;
         depth = m3.rec_n >> 16;
         rms = m3.rms;
-        const uint16_t *rec = reinterpret_cast<const uint16_t *>(stage) + (m3.rec_n & 0xffffu);
-        if (!(a.diag & 2u)) fold_sample(rec, cnt, fk, role, acc);
+        const uint32_t *rec = stage + (m3.rec_n & 0xffffu);
+        if (!(diag & 2u)) fold_sample(rec, cnt, fk, role, acc);
         else {
 #pragma unroll
             for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b];
@@ -1004,7 +1040,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
     for (int t = 0; t < 5; ++t) {
         int j, k;
         geno_jk((int)role * 5 + t, j, k);
-        mine[t] = (act && !(a.diag & 4u)) ? geno_p(j, k, es, fs, c, tot, a.m) : 0.0f;
+        mine[t] = (act && !(diag & 4u)) ? geno_p(j, k, es, fs, c, tot, a.m) : 0.0f;
     }
     float p[10];
 #pragma unroll
@@ -1015,7 +1051,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
     }
     if (act && role == 0u) {
         uint32_t lk[10], min_lk, rms_q, cns;
-        if (!(a.diag & 4u)) glf_finish(p, es, depth, rms, a.m, lk, min_lk, rms_q, cns);
+        if (!(diag & 4u)) glf_finish(p, es, depth, rms, a.m, lk, min_lk, rms_q, cns);
         else {
 #pragma unroll
             for (int g = 0; g < 10; ++g) lk[g] = (uint32_t)es[g & 3] & 0xffu;
@@ -1037,7 +1073,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
     wave_sync();
     if ((int)lane < G) {
         /* the decision reads both samples' records straight from LDS */
-        if (!(a.diag & 8u)) decide_site(a, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
+        if (!(diag & 8u)) decide_site(a, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
         else a.score[sites[lane]] = (int32_t)res[2 * lane].cns;
     }
     wave_sync();
@@ -1045,8 +1081,12 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
 
 }  // namespace
 
+/* DIAG = true only for the profiling ablations (SS_DIAG); the production
+ * instance has every ablation branch folded away. */
+template <bool DIAG>
 __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
 {
+    const uint32_t diag = DIAG ? a.diag : 0u;
     __shared__ double fk[256];
     __shared__ MainLds L;
     const uint32_t lane = lane_id();
@@ -1097,22 +1137,22 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
                 S2[m].bt = t_i - cur.t0;
                 S2[m].bn = cur.lt + (n_i - cur.n0);
                 S2[m].ref16 = rdesc >> 8;
-                tot[m] = S2[m].nt + S2[m].nn;
+                tot[m] = S2[m].nt + (S2[m].nt & 1u) + S2[m].nn;   /* sort slots incl. pad */
                 if (lane == 0 && i + (uint32_t)m < cur.b) {
                     sites[G + m] = (uint32_t)(blk * GB + j);
                     refcs[G + m] = rdesc & 0xffu;
                 }
             }
             if (i + 1u < cur.b && tot[0] <= 128u && tot[1] <= 128u) {
-                sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, a.diag);   /* two sites, interleaved */
+                sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, diag);   /* two sites, interleaved */
                 G += 2;
                 i += 2;
                 continue;
             }
             SiteA S1[1] = {S2[0]};
-            if (tot[0] <= 128u) sort_sites<1, 1>(stage, S1, cap, slot + 2 * G, a.diag);
-            else if (tot[0] <= 256u) sort_sites<2, 1>(stage, S1, cap, slot + 2 * G, a.diag);
-            else sort_sites<4, 1>(stage, S1, cap, slot + 2 * G, a.diag);
+            if (tot[0] <= 128u) sort_sites<1, 1>(stage, S1, cap, slot + 2 * G, diag);
+            else if (tot[0] <= 256u) sort_sites<2, 1>(stage, S1, cap, slot + 2 * G, diag);
+            else sort_sites<4, 1>(stage, S1, cap, slot + 2 * G, diag);
             ++G;
             ++i;
         }
@@ -1135,7 +1175,7 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
             have = nxt.a < nxt.b;
         }
         /* ---- phases B + C + D (the next DMA is issued after the fold) ---- */
-        finish_sub(a, G, stage, slot, res, sites, refcs, fk, have, nxt);
+        finish_sub(a, G, stage, slot, res, sites, refcs, fk, have, nxt, diag);
         if (!have) break;
         cur = nxt;
     }
@@ -1306,7 +1346,8 @@ int ss_launch_score(const ss_score_args &a, int main_grid, int deep_grid, hipStr
 {
     hipError_t e;
     if (ev0) (void)hipEventRecord(ev0, s);
-    hipLaunchKernelGGL(ss_score_main, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
+    if (a.diag) hipLaunchKernelGGL(ss_score_main<true>, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
+    else hipLaunchKernelGGL(ss_score_main<false>, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(ss_score_deep<false>, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);

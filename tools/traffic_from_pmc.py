@@ -11,6 +11,7 @@ import argparse
 import csv
 import json
 import os
+import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -19,7 +20,7 @@ def per_launch(path, counter, kernel):
     vals = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            if r["Counter_Name"] == counter and r["Kernel_Name"].startswith(kernel + "("):
+            if r["Counter_Name"] == counter and re.search(re.escape(kernel) + r"[<(]", r["Kernel_Name"]):
                 vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     assert vals, f"no {counter} rows for {kernel} in {path}"
     return sum(vals.values()) / len(vals), len(vals)
