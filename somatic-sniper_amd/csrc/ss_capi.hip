@@ -26,9 +26,7 @@ struct ss_ctx {
     int n_cu;
     ss_host_model_t hm;
     /* model on the device */
-    double *d_fk, *d_coef, *d_lhet;
-    int32_t *d_qadd, *d_prior, *d_jprior;
-    uint8_t *d_nt16;
+    uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
     uint32_t *d_counters;     /* [0] deep, [1] giant, [2] err, [3] scratch n_calls, [4] clamped */
     uint32_t *d_deep_list;
@@ -93,8 +91,7 @@ extern "C" void ss_ctx_destroy(ss_ctx_t *c)
     if (!c) return;
     hipSetDevice(c->device);
     hipDeviceSynchronize();
-    void *ptrs[] = {c->d_fk, c->d_coef, c->d_lhet, c->d_qadd, c->d_prior, c->d_jprior, c->d_nt16,
-                    c->d_counters, c->d_deep_list, c->d_giant_list, c->d_giant_scratch, c->d_stage,
+    void *ptrs[] = {c->d_tab, c->d_counters, c->d_deep_list, c->d_giant_list, c->d_giant_scratch, c->d_stage,
                     c->d_cdf, c->d_scan_tmp, c->d_depth_tmp};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -125,13 +122,23 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { ss_ctx_destroy(c); return SS_E_HIP; }
     c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
 #define TRY(x) do { if ((rc = (x)) != SS_OK) { ss_ctx_destroy(c); return rc; } } while (0)
-    TRY(upload(&c->d_fk, c->hm.fk, 256));
-    TRY(upload(&c->d_coef, c->hm.coef, (size_t)64 << 16));
-    TRY(upload(&c->d_lhet, c->hm.lhet, 65536));
-    TRY(upload(&c->d_qadd, c->hm.qadd, 1024));
-    TRY(upload(&c->d_prior, c->hm.prior, 160));
-    TRY(upload(&c->d_jprior, c->hm.jprior, 1600));
-    TRY(upload(&c->d_nt16, (const uint8_t *)ss_nt16_table, 256));
+    TRY(dev_alloc((void **)&c->d_tab, SS_TAB_BYTES));
+    {
+        struct { size_t off; const void *src; size_t n; } parts[] = {
+            {SS_TAB_COEF, c->hm.coef, ((size_t)64 << 16) * sizeof(double)},
+            {SS_TAB_LHET, c->hm.lhet, (size_t)65536 * sizeof(double)},
+            {SS_TAB_FK, c->hm.fk, 256 * sizeof(double)},
+            {SS_TAB_QADD, c->hm.qadd, 1024 * sizeof(int32_t)},
+            {SS_TAB_PRIOR, c->hm.prior, 160 * sizeof(int32_t)},
+            {SS_TAB_JPRIOR, c->hm.jprior, 1600 * sizeof(int32_t)},
+            {SS_TAB_NT16, ss_nt16_table, 256},
+        };
+        for (auto &pt : parts)
+            if (hipMemcpy(c->d_tab + pt.off, pt.src, pt.n, hipMemcpyHostToDevice) != hipSuccess) {
+                ss_ctx_destroy(c);
+                return SS_E_HIP;
+            }
+    }
     TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t)));
     c->giant_cap = 1u << 16;
     TRY(dev_alloc((void **)&c->d_giant_list, c->giant_cap * sizeof(uint32_t)));
@@ -231,19 +238,15 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         const char *dg = getenv("SS_DIAG");
         a.diag = dg ? (uint32_t)strtoul(dg, nullptr, 0) : 0u;
     }
-    a.m.fk = c->d_fk;
-    a.m.coef = c->d_coef;
-    a.m.lhet = c->d_lhet;
-    a.m.qadd = c->d_qadd;
-    a.m.prior = c->d_prior;
-    a.m.jprior = c->d_jprior;
-    a.m.nt16 = c->d_nt16;
+    a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;
-    a.m.cap_mapQ = c->hm.prm.cap_mapQ;
+    {   /* only min(mapQ & 0x7f, cap) is ever used (sniper_maqcns.c:173) */
+        const int cap = c->hm.prm.cap_mapQ;
+        a.m.cap_mapQ = cap < 0 ? 0 : (cap > 127 ? 127 : cap);
+    }
     a.m.min_somatic_qual = c->hm.prm.min_somatic_qual;
-    a.m.use_joint = c->hm.prm.use_joint_priors;
-    a.m.include_loh = c->hm.prm.include_loh;
-    a.m.include_gor = c->hm.prm.include_gor;
+    a.m.flags = (c->hm.prm.use_joint_priors ? SS_MF_JOINT : 0u) | (c->hm.prm.include_loh ? SS_MF_LOH : 0u) |
+                (c->hm.prm.include_gor ? SS_MF_GOR : 0u);
     /* main kernel: 4 waves per workgroup, one 16-site block per wave per
      * iteration, grid-strided; 4 workgroups fit a CU (LDS), so 16 per CU gives
      * each CU four rounds of waves for load balance */

@@ -10,22 +10,42 @@
 #include "sniper_amd.h"
 #include "ss_synth_core.h"
 
-/* Device copy of the model (built on the host by ss_tables.c). */
+/* Device copy of the model (built on the host by ss_tables.c): every table
+ * in ONE allocation, so a kernel needs a single base pointer (SGPR pressure). */
+#define SS_TAB_COEF   ((size_t)0)                                 /* f64 [64 << 16]  */
+#define SS_TAB_LHET   (SS_TAB_COEF + ((size_t)64 << 16) * 8)      /* f64 [65536]     */
+#define SS_TAB_FK     (SS_TAB_LHET + (size_t)65536 * 8)           /* f64 [256]       */
+#define SS_TAB_QADD   (SS_TAB_FK + (size_t)256 * 8)               /* i32 [1024]      */
+#define SS_TAB_PRIOR  (SS_TAB_QADD + (size_t)1024 * 4)            /* i32 [16 * 10]   */
+#define SS_TAB_JPRIOR (SS_TAB_PRIOR + (size_t)160 * 4)            /* i32 [16*10*10]  */
+#define SS_TAB_NT16   (SS_TAB_JPRIOR + (size_t)1600 * 4)          /* u8  [256]       */
+#define SS_TAB_BYTES  (SS_TAB_NT16 + (size_t)256)
+
+#define SS_MF_JOINT 1u
+#define SS_MF_LOH   2u
+#define SS_MF_GOR   4u
+
 struct ss_dev_model {
-    const double  *fk;       /* [256]            */
-    const double  *coef;     /* [64 << 16]       */
-    const double  *lhet;     /* [65536]          */
-    const int32_t *qadd;     /* [1024]           */
-    const int32_t *prior;    /* [16 * 10]        */
-    const int32_t *jprior;   /* [16 * 10 * 10]   */
-    const uint8_t *nt16;     /* [256]            */
-    int32_t q_r_int;
-    int32_t cap_mapQ;
-    int32_t min_somatic_qual;
-    int32_t use_joint;
-    int32_t include_loh;
-    int32_t include_gor;
+    const uint8_t *tab;      /* SS_TAB_* layout */
+    int32_t  q_r_int;
+    int32_t  cap_mapQ;       /* clamped to [0, 127]: only min(mapQ & 0x7f, cap) is used */
+    int32_t  min_somatic_qual;
+    uint32_t flags;          /* SS_MF_* */
 };
+
+#define SS_TAB_ACCESSOR(name, T, off)                                                  \
+    __host__ __device__ __forceinline__ const T *ss_tab_##name(const ss_dev_model &m) \
+    {                                                                                  \
+        return reinterpret_cast<const T *>(m.tab + (off));                             \
+    }
+SS_TAB_ACCESSOR(coef, double, SS_TAB_COEF)
+SS_TAB_ACCESSOR(lhet, double, SS_TAB_LHET)
+SS_TAB_ACCESSOR(fk, double, SS_TAB_FK)
+SS_TAB_ACCESSOR(qadd, int32_t, SS_TAB_QADD)
+SS_TAB_ACCESSOR(prior, int32_t, SS_TAB_PRIOR)
+SS_TAB_ACCESSOR(jprior, int32_t, SS_TAB_JPRIOR)
+SS_TAB_ACCESSOR(nt16, uint8_t, SS_TAB_NT16)
+#undef SS_TAB_ACCESSOR
 
 /* Per-launch arguments of the scoring kernels. */
 struct ss_score_args {

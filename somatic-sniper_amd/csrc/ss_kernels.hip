@@ -206,10 +206,10 @@ __device__ __forceinline__ float geno_p(int j, int k, const float es[4], const f
         c2 += use ? c[i] : 0u;
     }
     const bool hom = j == k;
-    const double lh = hom ? 0.0 : -4.343 * m.lhet[c[j] << 8 | c[k]];
+    const double lh = hom ? 0.0 : -4.343 * ss_tab_lhet(m)[c[j] << 8 | c[k]];
     float v;
     if (c2) {
-        const double cf = m.coef[(uint32_t)clamp_bar_e(e, f) << 16 | tot << 8 | c2];
+        const double cf = ss_tab_coef(m)[(uint32_t)clamp_bar_e(e, f) << 16 | tot << 8 | c2];
         v = hom ? (float)((double)e + cf) : (float)((lh + (double)e) + cf);
     } else {
         v = hom ? 0.0f : (float)lh;
@@ -337,7 +337,7 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
 {
     const ss_dev_model &m = a.m;
     const int rb = (int)refc;
-    const int rb4 = m.nt16[refc & 0xffu];
+    const int rb4 = ss_tab_nt16(m)[refc & 0xffu];
     if (!(rb != 'N' && rt.depth > 0u && rn.depth > 0u)) { a.score[site] = -1; return; }
     const uint32_t ct = rt.cns, cn = rn.cns;
     const int t1 = (int)(ct >> 28), t2 = (int)(ct >> 24 & 0xf), ts1 = (int)(ct >> 8 & 0xff), ts2 = (int)(ct & 0xff);
@@ -354,25 +354,25 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
         if (nq > 255) nq = 255;
     }
     int qps = 255, jt = 0, jn = 0, jcq = 255;
-    if (m.use_joint) {
+    if ((m.flags & SS_MF_JOINT)) {
         /* joint prior over (normal i, tumor j) with RAW glf lk (:180) */
         int marg = 255, best = 1000, bi = -1, bj = -1;
 #pragma unroll 1
         for (int i = 0; i < 10; ++i)
 #pragma unroll 1
             for (int j = 0; j < 10; ++j) {
-                int v = (int)rn.lk[i] + (int)rt.lk[j] + m.jprior[(rb4 * 10 + i) * 10 + j];
+                int v = (int)rn.lk[i] + (int)rt.lk[j] + ss_tab_jprior(m)[(rb4 * 10 + i) * 10 + j];
                 if (v > 255) v = 255;
                 if (v < best) { best = v; bi = i; bj = j; }
-                marg = qadd(m.qadd, marg, v, clamped);
+                marg = qadd(ss_tab_qadd(m), marg, v, clamped);
             }
 #pragma unroll 1
         for (int j = 0; j < 10; ++j) {
-            int v = (int)rn.lk[j] + (int)rt.lk[j] + m.jprior[(rb4 * 10 + j) * 10 + j];
+            int v = (int)rn.lk[j] + (int)rt.lk[j] + ss_tab_jprior(m)[(rb4 * 10 + j) * 10 + j];
             if (v > 255) v = 255;
             const int l = v - marg;
-            qps = qadd(m.qadd, qps, l, clamped);
-            if (j != bj) jcq = qadd(m.qadd, jcq, l, clamped);  /* stale-index quirk, :196 */
+            qps = qadd(ss_tab_qadd(m), qps, l, clamped);
+            if (j != bj) jcq = qadd(ss_tab_qadd(m), jcq, l, clamped);  /* stale-index quirk, :196 */
         }
         if (jcq > 255) jcq = 255;
         /* glfBase (somatic_sniper.c:26): genotype index -> nt16 bit set */
@@ -387,26 +387,26 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
         int st = 255, sn = 255;
 #pragma unroll 1
         for (int j = 0; j < 10; ++j) {
-            const int xt = (int)rt.lk[j] + m.prior[rb4 * 10 + j];
-            const int xn = (int)rn.lk[j] + m.prior[rb4 * 10 + j];
-            st = qadd(m.qadd, xt, st, clamped);
-            sn = qadd(m.qadd, xn, sn, clamped);
+            const int xt = (int)rt.lk[j] + ss_tab_prior(m)[rb4 * 10 + j];
+            const int xn = (int)rn.lk[j] + ss_tab_prior(m)[rb4 * 10 + j];
+            st = qadd(ss_tab_qadd(m), xt, st, clamped);
+            sn = qadd(ss_tab_qadd(m), xn, sn, clamped);
         }
 #pragma unroll 1
         for (int j = 0; j < 10; ++j) {
-            int vt = (int)rt.lk[j] + m.prior[rb4 * 10 + j] - st;
-            int vn = (int)rn.lk[j] + m.prior[rb4 * 10 + j] - sn;
+            int vt = (int)rt.lk[j] + ss_tab_prior(m)[rb4 * 10 + j] - st;
+            int vn = (int)rn.lk[j] + ss_tab_prior(m)[rb4 * 10 + j] - sn;
             if (vt > 255) vt = 255;
             if (vn > 255) vn = 255;
-            qps = qadd(m.qadd, qps, vt + vn, clamped);
+            qps = qadd(ss_tab_qadd(m), qps, vt + vn, clamped);
         }
     }
     a.score[site] = qps;
     if (clamped && a.n_clamped) atomicAdd(a.n_clamped, (uint32_t)clamped);
     const int tg = jt ? jt : t1, ng = jn ? jn : n1;
     const bool emit = m.min_somatic_qual <= qps &&
-                      (m.include_loh || !proper_subset(tg, ng)) &&
-                      (m.include_gor || !(!proper_subset(rb4, ng) && (tg & ~ng) == rb4));
+                      ((m.flags & SS_MF_LOH) || !proper_subset(tg, ng)) &&
+                      ((m.flags & SS_MF_GOR) || !(!proper_subset(rb4, ng) && (tg & ~ng) == rb4));
     if (!emit || !a.calls) return;
     const uint32_t slot = atomicAdd(a.n_calls, 1u);
     if (slot >= a.calls_cap) return;
@@ -488,7 +488,7 @@ __device__ __forceinline__ void finish_group(const ss_score_args &a, int G, cons
             r.rms_q = (uint8_t)rms_q;
             if (a.glf) {
                 const uint32_t site = sinfo[s].site;
-                const uint32_t ref16 = a.m.nt16[sinfo[s].refc & 0xffu];
+                const uint32_t ref16 = ss_tab_nt16(a.m)[sinfo[s].refc & 0xffu];
                 store_glf(&a.glf[2ull * site + (slot & 1)], ref16, lk, min_lk, rms_q, r.depth);
             }
         }
@@ -611,6 +611,13 @@ __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b)
 
 /* x from lane ^ LJ without an LDS round trip: DPP quad permutes for 1 and 2,
  * DPP row shifts for 4 and 8, v_permlane16/32_swap for 16 and 32. */
+#ifndef SS_XOR_BANK
+#define SS_XOR_BANK 1
+#endif
+#ifndef SS_CX_EXEC
+#define SS_CX_EXEC 0      /* exec-masked max measured slower (SALU exec writes) */
+#endif
+
 template <int LJ>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
 {
@@ -619,6 +626,15 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0xb1, 0xf, 0xf, false);  /* quad_perm 1,0,3,2 */
     } else if constexpr (LJ == 2) {
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x4e, 0xf, 0xf, false);  /* quad_perm 2,3,0,1 */
+#if SS_XOR_BANK
+    } else if constexpr (LJ == 4) {
+        /* banks 0,2 read lane + 4, banks 1,3 lane - 4: two bank-masked moves */
+        const int up = __builtin_amdgcn_update_dpp(0, xi, 0x104, 0xf, 0x5, false);  /* row_shl:4 */
+        return (uint32_t)__builtin_amdgcn_update_dpp(up, xi, 0x114, 0xf, 0xa, false); /* row_shr:4 */
+    } else if constexpr (LJ == 8) {
+        const int up = __builtin_amdgcn_update_dpp(0, xi, 0x108, 0xf, 0x3, false);  /* row_shl:8 */
+        return (uint32_t)__builtin_amdgcn_update_dpp(up, xi, 0x118, 0xf, 0xc, false); /* row_shr:8 */
+#else
     } else if constexpr (LJ == 4) {
         const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x104, 0xf, 0xf, false); /* row_shl:4 */
         const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x114, 0xf, 0xf, false); /* row_shr:4 */
@@ -627,6 +643,7 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
         const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x108, 0xf, 0xf, false); /* row_shl:8 */
         const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x118, 0xf, 0xf, false); /* row_shr:8 */
         return (lane_id() & 8u) ? dn : up;
+#endif
     } else if constexpr (LJ == 16) {
         const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
         return (lane_id() & 16u) ? r[0] : r[1];
@@ -656,6 +673,81 @@ __device__ __forceinline__ uint32_t halfswap(uint32_t x) { return (x >> 16) | (x
 /* half cleaners e <-> e ^ j for j = J, J/2, ..., 1 (compile-time recursion);
  * M independent networks are advanced together so their dependency chains
  * (and DPP wait states) interleave. */
+/* Cross-lane compare-exchange of packed u16 pairs: lanes with bit LJ clear
+ * keep min(x, o), lanes with it set keep max(x, o).  The max is issued under
+ * an exec mask (2 VALU instead of min + max + select; no lane-mask SGPRs to
+ * keep live across the network).  All lanes must be active on entry. */
+template <int LJ>
+__device__ __forceinline__ uint32_t cx_lanes(uint32_t x, uint32_t o)
+{
+#if !SS_CX_EXEC
+    return (lane_id() & (uint32_t)LJ) ? pk_max(x, o) : pk_min(x, o);
+#endif
+    uint32_t r;
+    uint64_t saved;
+    if constexpr (LJ == 32) {
+        asm volatile("v_pk_min_u16 %0, %2, %3\n\t"
+                     "s_mov_b64 %1, exec\n\t"
+                     "s_mov_b32 exec_lo, 0\n\t"
+                     "v_pk_max_u16 %0, %2, %3\n\t"
+                     "s_mov_b64 exec, %1"
+                     : "=&v"(r), "=&s"(saved)
+                     : "v"(x), "v"(o));
+    } else {
+        constexpr uint32_t pat = LJ == 1 ? 0xaaaaaaaau : LJ == 2 ? 0xccccccccu : LJ == 4 ? 0xf0f0f0f0u
+                               : LJ == 8 ? 0xff00ff00u : 0xffff0000u;
+        static_assert(LJ == 1 || LJ == 2 || LJ == 4 || LJ == 8 || LJ == 16, "lane bit");
+        asm volatile("v_pk_min_u16 %0, %2, %3\n\t"
+                     "s_mov_b64 %1, exec\n\t"
+                     "s_and_b32 exec_lo, exec_lo, %4\n\t"
+                     "s_and_b32 exec_hi, exec_hi, %4\n\t"
+                     "v_pk_max_u16 %0, %2, %3\n\t"
+                     "s_mov_b64 exec, %1"
+                     : "=&v"(r), "=&s"(saved)
+                     : "v"(x), "v"(o), "i"(pat));
+    }
+    return r;
+}
+
+/* In-register compare-exchange of the two halves: lo = min, hi = max, by two
+ * SDWA word ops instead of swap + min + max + merge.  The second op reads the
+ * first one's result through dst_unused:UNUSED_PRESERVE; back to back that
+ * read is stale on gfx950 (measured), so either one independent instruction
+ * (cx_halves2: two registers interleaved) or one wait state separates them. */
+__device__ __forceinline__ uint32_t cx_halves(uint32_t x)
+{
+    uint32_t r;
+    asm volatile("v_max_u16_sdwa %0, %1, %1 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                 "s_nop 0\n\t"
+                 "v_min_u16_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1"
+                 : "=&v"(r)
+                 : "v"(x));
+    return r;
+}
+
+__device__ __forceinline__ void cx_halves2(uint32_t &x0, uint32_t &x1)
+{
+    uint32_t r0, r1;
+    asm volatile("v_max_u16_sdwa %0, %2, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                 "v_max_u16_sdwa %1, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                 "v_min_u16_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
+                 "v_min_u16_sdwa %1, %3, %3 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1"
+                 : "=&v"(r0), "=&v"(r1)
+                 : "v"(x0), "v"(x1));
+    x0 = r0;
+    x1 = r1;
+}
+
+/* cx_halves over every register of the M x K set, two at a time */
+template <int M, int K>
+__device__ __forceinline__ void halves_all(uint32_t (&v)[M][K])
+{
+    constexpr int N = M * K;
+#pragma unroll
+    for (int i = 0; i + 1 < N; i += 2) cx_halves2(v[i / K][i % K], v[(i + 1) / K][(i + 1) % K]);
+    if constexpr (N & 1) v[M - 1][K - 1] = cx_halves(v[M - 1][K - 1]);
+}
+
 template <int M, int K, uint32_t J>
 __device__ __forceinline__ void half_clean(uint32_t (&v)[M][K])
 {
@@ -665,13 +757,12 @@ __device__ __forceinline__ void half_clean(uint32_t (&v)[M][K])
     } else {
         if constexpr (J >= E) {
             constexpr uint32_t lj = J / E;
-            const bool lower = (lane_id() & lj) == 0u;
 #pragma unroll
             for (int m = 0; m < M; ++m)
 #pragma unroll
                 for (int r = 0; r < K; ++r) {
                     const uint32_t o = xor_lane<(int)lj>(v[m][r]);
-                    v[m][r] = lower ? pk_min(v[m][r], o) : pk_max(v[m][r], o);
+                    v[m][r] = cx_lanes<(int)lj>(v[m][r], o);
                 }
         } else if constexpr (J >= 2u) {
 #pragma unroll
@@ -686,14 +777,7 @@ __device__ __forceinline__ void half_clean(uint32_t (&v)[M][K])
                     }
                 }
         } else {
-#pragma unroll
-            for (int m = 0; m < M; ++m)
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    const uint32_t sw = halfswap(v[m][r]);
-                    const uint32_t mn = pk_min(v[m][r], sw), mx = pk_max(v[m][r], sw);
-                    v[m][r] = (mn & 0xffffu) | (mx & 0xffff0000u);
-                }
+            halves_all<M, K>(v);
         }
         half_clean<M, K, (J >> 1)>(v);
     }
@@ -706,9 +790,10 @@ template <int M, int K, uint32_t k>
 __device__ __forceinline__ void flip_stage(uint32_t (&v)[M][K])
 {
     constexpr uint32_t E = 2u * K;
-    const uint32_t lane = lane_id();
     /* mirror: e <-> e ^ (k-1) */
-    if constexpr (k <= E) {
+    if constexpr (k == 2) {
+        halves_all<M, K>(v);                              /* e <-> e ^ 1: the two halves */
+    } else if constexpr (k <= E) {
 #pragma unroll
         for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -719,22 +804,18 @@ __device__ __forceinline__ void flip_stage(uint32_t (&v)[M][K])
                     const uint32_t mn = pk_min(v[m][r], sw), mx = pk_max(v[m][r], sw);
                     v[m][r] = mn;
                     v[m][r2] = halfswap(mx);
-                } else if (r2 == r) {
-                    const uint32_t sw = halfswap(v[m][r]);
-                    const uint32_t mn = pk_min(v[m][r], sw), mx = pk_max(v[m][r], sw);
-                    v[m][r] = (mn & 0xffffu) | (mx & 0xffff0000u);
                 }
             }
     } else {
         constexpr uint32_t mx_lane = k / E - 1u;          /* lane xor of the mirror */
-        const bool lower = (lane & ((mx_lane + 1u) >> 1)) == 0u;
+        constexpr int lbit = (int)((mx_lane + 1u) >> 1);    /* lanes with it set keep the max */
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             uint32_t nv[K];
 #pragma unroll
             for (int r = 0; r < K; ++r) {
                 const uint32_t o = halfswap(xor_lane<(int)mx_lane>(v[m][K - 1 - r]));
-                nv[r] = lower ? pk_min(v[m][r], o) : pk_max(v[m][r], o);
+                nv[r] = cx_lanes<lbit>(v[m][r], o);
             }
 #pragma unroll
             for (int r = 0; r < K; ++r) v[m][r] = nv[r];
@@ -923,7 +1004,7 @@ __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s
     } else if (lane < 33u) {
         if (s + (lane - 17u) < a.n_sites) {
             const uint32_t rc = a.ref[s + (lane - 17u)];
-            v = rc | (uint32_t)a.m.nt16[rc] << 8;
+            v = rc | (uint32_t)ss_tab_nt16(a.m)[rc] << 8;
         }
     } else if (lane < 50u) {
         if (s + (lane - 33u) <= a.n_sites) v = a.off_n[s + (lane - 33u)];
@@ -1066,7 +1147,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
         r.depth = depth;
         if (a.glf) {
             const uint32_t s = (uint32_t)sl >> 1;
-            store_glf(&a.glf[2ull * sites[s] + (sl & 1)], a.m.nt16[refcs[s] & 0xffu], lk, min_lk,
+            store_glf(&a.glf[2ull * sites[s] + (sl & 1)], ss_tab_nt16(a.m)[refcs[s] & 0xffu], lk, min_lk,
                       rms_q, depth);
         }
     }
@@ -1091,7 +1172,7 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
     __shared__ MainLds L;
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6;
-    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = a.m.fk[i];
+    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
 
     uint32_t *stage = L.stage[wv];
@@ -1256,7 +1337,7 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
     __shared__ double fk[256];
     __shared__ DeepLds D;
     __shared__ uint32_t lbuf[GIANT ? 1 : 2][GIANT ? 1 : SS_DEEP_MAXN];
-    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = a.m.fk[i];
+    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
     const uint32_t count = GIANT ? *a.giant_count : *a.deep_count;
     const uint32_t lim = GIANT ? (count < a.giant_cap ? count : a.giant_cap)
@@ -1290,7 +1371,7 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
             continue;
         }
         const uint32_t refc = a.ref[s];
-        const uint32_t ref16 = a.m.nt16[refc];
+        const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
         if (threadIdx.x == 0) { D.sinfo[0].site = s; D.sinfo[0].refc = refc; }
         deep_sample(a.reads_t + ot, nt, ref16, cap, bt, D, 0);
         deep_sample(a.reads_n + on, nn, ref16, cap, bn, D, 1);

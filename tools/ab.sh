@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B: quick parity + main-kernel time for each variant library build/libsniper_amd_<V>.so
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p "$R/gpurun_out/ab"
+for V in "$@"; do
+  L=$R/somatic-sniper_amd/build/libsniper_amd_$V.so
+  SNIPER_AMD_LIB=$L timeout -k 10 200 python "$R/tools/quick_parity.py" > "$R/gpurun_out/ab/qp_$V.log" 2>&1 || { echo "$V parity run failed"; exit 1; }
+  SNIPER_AMD_LIB=$L timeout -k 10 200 python "$R/tools/ablate.py" --masks 0 --reps 10 > "$R/gpurun_out/ab/t_$V.log" 2>&1 || { echo "$V timing failed"; exit 1; }
+  echo "$V $(tail -n 1 $R/gpurun_out/ab/qp_$V.log) $(grep 'mask  0' $R/gpurun_out/ab/t_$V.log)"
+done
