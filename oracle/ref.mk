@@ -30,7 +30,7 @@ SNIPSRC  := sniper_maqcns.c somatic_sniper.c allele_util.c dqstats.c \
 HARNESS  := $(CURDIR)/oracle/ref_harness.c
 SYNTH    := $(CURDIR)/somatic-sniper_amd/csrc/ss_synth.c
 
-all: $(OUT)/bam-somaticsniper $(OUT)/ref_harness
+all: $(OUT)/bam-somaticsniper $(OUT)/ref_harness $(OUT)/bam-somaticsniper-dump
 
 $(SAMDIR)/.unpacked: $(REF)/vendor/samtools-0.1.6.tar.gz
 	mkdir -p $(SCRATCH)
@@ -57,6 +57,15 @@ $(OUT)/ref_harness: $(SCRATCH)/libbam.a $(HARNESS) $(SYNTH)
 	mkdir -p $(OUT)
 	$(CC) $(CFLAGS) $(INC) -I$(CURDIR)/somatic-sniper_amd/csrc -I$(CURDIR)/include \
 	  -o $@ $(HARNESS) $(SYNTH) $(addprefix $(SNIPER)/,$(SNIPSRC)) $(SCRATCH)/libbam.a -lz -lm
+
+# the reference CLI with a glf_somatic wrapper that dumps every site it is
+# handed (pileup parity test of the native CLI, tests/test_cli_native.py)
+$(OUT)/bam-somaticsniper-dump: $(SCRATCH)/libbam.a $(SCRATCH)/ver/version.h $(CURDIR)/oracle/pileup_dump_shim.c
+	mkdir -p $(OUT)/dumpobj
+	$(CC) $(CFLAGS) $(INC) -c $(REF)/src/exe/bam-somaticsniper/main.c -o $(OUT)/dumpobj/main.o
+	$(CC) $(CFLAGS) $(INC) -I$(CURDIR)/include -c $(CURDIR)/oracle/pileup_dump_shim.c -o $(OUT)/dumpobj/shim.o
+	$(CC) $(CFLAGS) $(INC) -o $@ $(OUT)/dumpobj/main.o $(OUT)/dumpobj/shim.o \
+	  $(addprefix $(SNIPER)/,$(SNIPSRC)) $(SCRATCH)/libbam.a -Wl,--wrap=glf_somatic -lz -lm
 
 clean:
 	rm -rf $(OUT)

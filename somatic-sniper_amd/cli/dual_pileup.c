@@ -1,0 +1,197 @@
+/* dual_pileup.c -- see dual_pileup.h for the behaviour being reproduced. */
+#include "dual_pileup.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct pl_node {
+    bam_record_t b;
+    uint32_t beg, end;
+    struct pl_node *next;
+} pl_node_t;
+
+typedef struct {
+    /* list of loaded reads; `tail` is always a spare node that receives the
+     * next record, so an empty list has head == tail, and head->b is then the
+     * last record that passed the filters (whether it was kept or not) */
+    pl_node_t *head, *tail, *spare;
+    pl_node_t *free_list;
+    int32_t tid, pos, max_tid, max_pos;
+    int is_eof, started;
+    uint32_t flag_mask;
+    int mapq_thresh;
+    pl_entry_t *pu;
+    int max_pu;
+    bgzf_reader_t *fp;
+    bam_record_t rec;          /* read buffer */
+    int error;
+} walker_t;
+
+static pl_node_t *node_new(walker_t *w)
+{
+    pl_node_t *p = w->free_list;
+    if (p) {
+        w->free_list = p->next;
+        p->next = NULL;
+        return p;
+    }
+    p = (pl_node_t *)calloc(1, sizeof *p);
+    if (!p) { fprintf(stderr, "out of memory\n"); exit(1); }
+    return p;
+}
+
+static void node_free(walker_t *w, pl_node_t *p)
+{
+    p->next = w->free_list;
+    w->free_list = p;
+}
+
+/* Position `pos` within read b: query offset and deletion flag, or 0 when
+ * the read does not contribute there (reference skip; resolve_cigar :59-111). */
+static int locate(const bam_record_t *b, uint32_t pos, int32_t *qpos, uint8_t *is_del)
+{
+    const uint32_t *cig = bam_rec_cigar(b);
+    uint32_t x = (uint32_t)b->pos, y = 0;
+    int keep = 1;
+    *qpos = -1;
+    *is_del = 0;
+    for (int k = 0; k < b->n_cigar; ++k) {
+        const uint32_t op = cig[k] & 0xf, l = cig[k] >> 4;
+        if (op == SS_CIG_M) {
+            if (x + l > pos) { *is_del = 0; *qpos = (int32_t)(y + (pos - x)); }
+            x += l;
+            y += l;
+        } else if (op == SS_CIG_D) {
+            if (x + l > pos) { *is_del = 1; *qpos = (int32_t)(y + (pos - x)); }
+            x += l;
+        } else if (op == SS_CIG_N) {
+            x += l;
+        } else if (op == SS_CIG_I || op == SS_CIG_S) {
+            y += l;
+        }
+        if (x > pos) {
+            if (op == SS_CIG_N) keep = 0;
+            break;
+        }
+    }
+    if (x <= pos) {
+        fprintf(stderr, "[bam_pileup] read %.*s does not cover position %u (CIGAR operations the "
+                        "pileup does not model). Abort!\n", (int)b->l_qname, (const char *)b->data, pos);
+        abort();
+    }
+    return keep;
+}
+
+static void walker_init(walker_t *w, bgzf_reader_t *fp, int mask, int thresh)
+{
+    memset(w, 0, sizeof *w);
+    w->fp = fp;
+    w->head = w->tail = node_new(w);
+    w->spare = node_new(w);
+    w->max_tid = w->max_pos = -1;
+    w->flag_mask = mask < 0 ? SS_BAM_DEF_MASK : (SS_BAM_FUNMAP | (uint32_t)mask);
+    w->mapq_thresh = thresh < 0 ? 0 : thresh;
+}
+
+static void walker_free(walker_t *w)
+{
+    pl_node_t *p = w->head;
+    while (p) { pl_node_t *q = p->next; bam_record_free(&p->b); free(p); p = q; }
+    if (w->spare) { bam_record_free(&w->spare->b); free(w->spare); }
+    p = w->free_list;
+    while (p) { pl_node_t *q = p->next; bam_record_free(&p->b); free(p); p = q; }
+    bam_record_free(&w->rec);
+    free(w->pu);
+}
+
+/* One step of the walk (get_next_pos): advance to the next position and
+ * return its number of pileup entries (>= 0), or -1 when the file is done. */
+static int next_pos(walker_t *w)
+{
+    if (w->max_pos != -1) {
+        if (w->tid < w->head->b.tid) { w->tid = w->head->b.tid; w->pos = 0; }
+        else ++w->pos;
+    }
+    if (w->is_eof && w->head->next == NULL) return -1;
+    for (;;) {
+        if (w->is_eof || w->max_tid > w->tid || (w->max_tid == w->tid && w->max_pos > w->pos)) {
+            int n = 0;
+            pl_node_t *q = w->spare;           /* stands in front of head */
+            q->next = w->head;
+            for (pl_node_t *p = w->head; p->next; q = p, p = p->next) {
+                if (p->b.tid < w->tid || (p->b.tid == w->tid && p->end <= (uint32_t)w->pos)) {
+                    q->next = p->next;
+                    node_free(w, p);
+                    p = q;
+                } else if (p->b.tid == w->tid && p->beg <= (uint32_t)w->pos) {
+                    if (n == w->max_pu) {
+                        w->max_pu = w->max_pu ? w->max_pu << 1 : 256;
+                        w->pu = (pl_entry_t *)realloc(w->pu, sizeof(pl_entry_t) * (size_t)w->max_pu);
+                        if (!w->pu) { fprintf(stderr, "out of memory\n"); exit(1); }
+                    }
+                    pl_entry_t *e = &w->pu[n];
+                    e->b = &p->b;
+                    if (!(p->b.flag & SS_BAM_FUNMAP) && locate(&p->b, (uint32_t)w->pos, &e->qpos, &e->is_del))
+                        ++n;
+                }
+            }
+            w->head = w->spare->next;
+            w->spare->next = NULL;
+            return n;
+        }
+        const int rc = bam_record_read(w->fp, &w->rec);
+        if (rc > 0) {
+            if (!(w->rec.flag & w->flag_mask) && !(w->rec.mapq < w->mapq_thresh)) {
+                bam_record_copy(&w->tail->b, &w->rec);
+                w->tail->beg = (uint32_t)w->rec.pos;
+                w->tail->end = bam_rec_end(&w->rec);
+                if (w->rec.tid < w->max_tid) {
+                    fprintf(stderr, "[bam_pileup_core] the input is not sorted. Abort!\n");
+                    abort();
+                }
+                w->max_tid = w->rec.tid;
+                w->max_pos = (int32_t)w->tail->beg;
+                if (w->tail->end > (uint32_t)w->pos) {
+                    w->tail->next = node_new(w);
+                    w->tail = w->tail->next;
+                }
+            }
+        } else {
+            if (rc < 0) w->error = 1;
+            w->is_eof = 1;
+        }
+    }
+}
+
+int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, dual_site_fn fn,
+                    void *data)
+{
+    walker_t *w1 = (walker_t *)malloc(sizeof(walker_t)), *w2 = (walker_t *)malloc(sizeof(walker_t));
+    if (!w1 || !w2) { free(w1); free(w2); return -1; }
+    walker_init(w1, fp1, mask, thresh);
+    walker_init(w2, fp2, mask, thresh);
+    int r1 = -1, r2 = -1, stop = 0;
+    while (!stop && (r1 = next_pos(w1)) >= 0 && (r2 = next_pos(w2)) >= 0) {
+        do {
+            if (w2->tid > w1->tid)
+                while (w2->tid > w1->tid && (r1 = next_pos(w1)) >= 0) {}
+            if (w1->tid > w2->tid)
+                while (w2->tid < w1->tid && (r2 = next_pos(w2)) >= 0) {}
+        } while (w2->tid != w1->tid && r1 >= 0 && r2 >= 0);
+        if (r1 > 0 && r2 > 0) {
+            if (w1->tid != w2->tid || w1->pos != w2->pos) {
+                fprintf(stderr, "[dual_pileup] tumor and normal walks out of step. Abort!\n");
+                abort();
+            }
+            stop = fn(w1->tid, w1->pos, r1, r2, w1->pu, w2->pu, data);
+        }
+    }
+    const int err = w1->error || w2->error;
+    if (err) fprintf(stderr, "[dual_pileup] truncated or malformed BAM record\n");
+    walker_free(w1);
+    walker_free(w2);
+    free(w1);
+    free(w2);
+    return err ? -1 : 0;
+}

@@ -1,0 +1,397 @@
+/*
+ * sniper_cli.c -- bam-somaticsniper, MI355X build.
+ *
+ * Command line, messages and outputs follow the reference CLI
+ * (src/exe/bam-somaticsniper/main.c:27-162); the site walk is dual_pileup.c
+ * (sniper_pileup.c restated), the per-site scoring is the C ABI
+ * (include/sniper_amd.h) on the GPU, fed in batches by this file:
+ *
+ *   pileup thread                      scoring thread
+ *   ----------------------------       -------------------------------------
+ *   pack sites into batch k      ->    ss_score_batch_host(batch k)
+ *   (while k-1 is being scored)        dqstats + writer for every emitted
+ *                                      site, in (tid, pos) order
+ *
+ * A site is what glf_somatic (somatic_sniper.c:109) sees: the ref char of
+ * the cached contig (fai fetch, :112-117) and the non-deleted, mapped reads of
+ * both samples (sniper_maqcns.c:147).  There is no CPU scoring path: without a
+ * usable GPU the program stops with an error.
+ *
+ * Environment: SS_DEVICE (GPU index, default 0), SS_BATCH (sites per batch,
+ * default 2^20), SS_BGZF_THREADS (inflate threads per BAM, default 4),
+ * SS_DUMP_PILEUP=FILE (test hook: also write every reported site, see
+ * dump_site()), SS_PILEUP_ONLY=1 (test hook with SS_DUMP_PILEUP: walk and dump
+ * without scoring, so the pileup restatement is testable on a host without a
+ * GPU; no output records are written).
+ */
+#include <getopt.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "bam_reader.h"
+#include "bgzf_reader.h"
+#include "dual_pileup.h"
+#include "fasta_index.h"
+#include "sniper_amd.h"
+#include "sniper_output.h"
+
+#ifndef SS_CLI_VERSION
+#define SS_CLI_VERSION "mi355x-1.0"
+#endif
+#ifndef SS_CLI_COMMIT
+#define SS_CLI_COMMIT "unknown"
+#endif
+
+/* ---- batches --------------------------------------------------------- */
+typedef struct {
+    size_t n, cap;
+    size_t nt, capt, nn, capn;
+    uint8_t *ref;
+    uint32_t *off_t, *off_n, *reads_t, *reads_n, *tid, *pos;
+    int32_t *score;
+    ss_call_t *calls;
+    size_t calls_cap;
+} batch_t;
+
+static void *xrealloc(void *p, size_t n)
+{
+    void *q = realloc(p, n ? n : 1);
+    if (!q) { fprintf(stderr, "out of memory\n"); exit(1); }
+    return q;
+}
+
+static void batch_init(batch_t *b, size_t cap)
+{
+    memset(b, 0, sizeof *b);
+    b->cap = cap;
+    b->ref = (uint8_t *)xrealloc(NULL, cap);
+    b->off_t = (uint32_t *)xrealloc(NULL, (cap + 1) * 4);
+    b->off_n = (uint32_t *)xrealloc(NULL, (cap + 1) * 4);
+    b->tid = (uint32_t *)xrealloc(NULL, cap * 4);
+    b->pos = (uint32_t *)xrealloc(NULL, cap * 4);
+    b->score = (int32_t *)xrealloc(NULL, cap * 4);
+    b->calls_cap = 4096;
+    b->calls = (ss_call_t *)xrealloc(NULL, b->calls_cap * sizeof(ss_call_t));
+    b->off_t[0] = b->off_n[0] = 0;
+}
+
+static void batch_free(batch_t *b)
+{
+    free(b->ref); free(b->off_t); free(b->off_n); free(b->reads_t); free(b->reads_n);
+    free(b->tid); free(b->pos); free(b->score); free(b->calls);
+}
+
+/* ---- run state --------------------------------------------------------- */
+typedef struct {
+    /* reference */
+    fasta_index_t *fai;
+    bam_header_t *h1;
+    int cur_tid, cur_len;
+    char *cur_ref;
+    /* scoring */
+    ss_ctx_t *ctx;
+    FILE *out;
+    int fmt;
+    batch_t bat[2];
+    int fill;                 /* batch being filled by the pileup thread */
+    int pending;              /* batch index handed to the scorer, -1 none */
+    int quit, failed;
+    pthread_t th;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    FILE *dump;
+    int pileup_only;
+} run_t;
+
+static void emit_batch(run_t *R, batch_t *b)
+{
+    ss_batch_t in = {b->n, b->ref, b->off_t, b->off_n, b->reads_t, b->reads_n};
+    uint32_t ncalls = 0, nclamp = 0;
+    for (;;) {
+        ss_out_t o = {b->score, b->calls, (uint32_t)b->calls_cap, &ncalls, NULL, &nclamp};
+        const int rc = ss_score_batch_host(R->ctx, &in, &o);
+        if (rc == SS_E_CAPACITY && ncalls > b->calls_cap) {
+            b->calls_cap = ncalls;
+            b->calls = (ss_call_t *)xrealloc(b->calls, b->calls_cap * sizeof(ss_call_t));
+            continue;
+        }
+        if (rc) {
+            fprintf(stderr, "[bam-somaticsniper] GPU scoring failed: %s\n", ss_strerror(rc));
+            R->failed = 1;
+            return;
+        }
+        break;
+    }
+    for (uint32_t i = 0; i < ncalls; ++i) {
+        const ss_call_t *c = &b->calls[i];
+        const uint32_t s = c->site;
+        ss_site_out_t o;
+        memset(&o, 0, sizeof o);
+        o.seq_name = R->h1->name[b->tid[s]];
+        o.pos = b->pos[s];
+        o.ref_base = b->ref[s];
+        o.ref_base4 = c->ref_base4;
+        const int tb = (int)(c->cns_tumor >> 28), nb = (int)(c->cns_normal >> 28);
+        const int tg = c->joint_gt_tumor ? c->joint_gt_tumor : tb;
+        const int ng = c->joint_gt_normal ? c->joint_gt_normal : nb;
+        o.tumor.genotype = tb;
+        o.tumor.consensus_quality = (int)(c->cns_tumor >> 8 & 0xff);
+        o.tumor.variant_allele_quality = c->snp_q_tumor;
+        o.tumor.somatic_score = c->somatic_score;
+        o.tumor.joint_genotype = c->joint_gt_tumor;
+        o.tumor.joint_consensus_quality = c->joint_cq;
+        o.tumor.variant_status = c->status_tumor;
+        ss_dqstats_packed(b->reads_t + b->off_t[s], b->off_t[s + 1] - b->off_t[s], o.ref_base4,
+                          (uint32_t)(o.ref_base4 | tg | ng), &o.tumor.dq);
+        o.normal.genotype = nb;
+        o.normal.consensus_quality = (int)(c->cns_normal >> 8 & 0xff);
+        o.normal.variant_allele_quality = c->snp_q_normal;
+        o.normal.somatic_score = -1;
+        o.normal.joint_genotype = c->joint_gt_normal;
+        o.normal.joint_consensus_quality = c->joint_cq;
+        o.normal.variant_status = c->status_normal;
+        ss_dqstats_packed(b->reads_n + b->off_n[s], b->off_n[s + 1] - b->off_n[s], o.ref_base4,
+                          (uint32_t)(o.ref_base4 | ng | tg), &o.normal.dq);
+        ss_write_site(R->out, R->fmt, &o);
+    }
+}
+
+static void *scorer_main(void *arg)
+{
+    run_t *R = (run_t *)arg;
+    pthread_mutex_lock(&R->mu);
+    for (;;) {
+        while (R->pending < 0 && !R->quit) pthread_cond_wait(&R->cv, &R->mu);
+        if (R->pending < 0 && R->quit) break;
+        batch_t *b = &R->bat[R->pending];
+        pthread_mutex_unlock(&R->mu);
+        if (!R->failed) emit_batch(R, b);
+        b->n = b->nt = b->nn = 0;
+        pthread_mutex_lock(&R->mu);
+        R->pending = -1;
+        pthread_cond_broadcast(&R->cv);
+    }
+    pthread_mutex_unlock(&R->mu);
+    return NULL;
+}
+
+/* hand the filled batch to the scorer; continue in the other buffer */
+static void submit(run_t *R)
+{
+    pthread_mutex_lock(&R->mu);
+    while (R->pending >= 0) pthread_cond_wait(&R->cv, &R->mu);
+    R->pending = R->fill;
+    R->fill ^= 1;
+    pthread_cond_broadcast(&R->cv);
+    pthread_mutex_unlock(&R->mu);
+}
+
+static void pack(batch_t *b, const pl_entry_t *pu, int n, int tumor)
+{
+    uint32_t **dst = tumor ? &b->reads_t : &b->reads_n;
+    size_t *len = tumor ? &b->nt : &b->nn, *cap = tumor ? &b->capt : &b->capn;
+    if (*len + (size_t)n > *cap) {
+        size_t c = *cap ? *cap : 1 << 20;
+        while (c < *len + (size_t)n) c *= 2;
+        *dst = (uint32_t *)xrealloc(*dst, c * 4);
+        *cap = c;
+    }
+    uint32_t *o = *dst + *len;
+    size_t k = 0;
+    for (int i = 0; i < n; ++i) {
+        const pl_entry_t *e = &pu[i];
+        if (e->is_del || (e->b->flag & SS_BAM_FUNMAP)) continue;
+        o[k++] = SS_READ_PACK(e->b->mapq, bam_rec_qual(e->b)[e->qpos], bam_rec_base(e->b, e->qpos),
+                              (e->b->flag & SS_BAM_FREVERSE) ? 1u : 0u);
+    }
+    *len += k;
+}
+
+/* test hook: tid pos n1 n2 refchar | tumor packed reads | normal packed reads */
+static void dump_site(run_t *R, const batch_t *b, size_t s, int n1, int n2)
+{
+    fprintf(R->dump, "%u\t%u\t%d\t%d\t%d\t", b->tid[s], b->pos[s], n1, n2, b->ref[s]);
+    for (uint32_t i = b->off_t[s]; i < b->off_t[s + 1]; ++i) fprintf(R->dump, "%x,", b->reads_t[i]);
+    fputc('\t', R->dump);
+    for (uint32_t i = b->off_n[s]; i < b->off_n[s + 1]; ++i) fprintf(R->dump, "%x,", b->reads_n[i]);
+    fputc('\n', R->dump);
+}
+
+static int on_site(int32_t tid, int32_t pos, int n1, int n2, const pl_entry_t *pu1, const pl_entry_t *pu2,
+                   void *data)
+{
+    run_t *R = (run_t *)data;
+    if (R->fai && tid != R->cur_tid) {          /* contig cache (somatic_sniper.c:112-117) */
+        free(R->cur_ref);
+        R->cur_ref = fasta_fetch(R->fai, R->h1->name[tid], &R->cur_len);
+        R->cur_tid = tid;
+    }
+    batch_t *b = &R->bat[R->fill];
+    const size_t s = b->n;
+    b->ref[s] = (uint8_t)((R->cur_ref && pos < R->cur_len) ? R->cur_ref[pos] : 'N');
+    b->tid[s] = (uint32_t)tid;
+    b->pos[s] = (uint32_t)pos;
+    pack(b, pu1, n1, 1);
+    pack(b, pu2, n2, 0);
+    b->off_t[s + 1] = (uint32_t)b->nt;
+    b->off_n[s + 1] = (uint32_t)b->nn;
+    b->n = s + 1;
+    if (R->dump) dump_site(R, b, s, n1, n2);
+    if (R->pileup_only) {                       /* test hook: nothing is scored */
+        b->n = b->nt = b->nn = 0;
+        return 0;
+    }
+    if (b->n == b->cap || b->nt > 0xC0000000u || b->nn > 0xC0000000u) submit(R);
+    return R->failed;
+}
+
+/* ---- command line --------------------------------------------------------- */
+static void version_info(void)
+{
+    printf("Somatic Sniper version (%s) (commit %s)\n", SS_CLI_VERSION, SS_CLI_COMMIT);
+}
+
+static void usage(const char *progname, const ss_params_t *p, int mapq)
+{
+    const char *pn = strrchr(progname, '/');
+    pn = pn ? pn + 1 : progname;
+    fprintf(stderr, "\n\n%s [options] -f <ref.fasta> <tumor.bam> <normal.bam> <snp_output_file>\n\n", pn);
+    fprintf(stderr, "Required Option: \n");
+    fprintf(stderr, "        -f FILE   REQUIRED reference sequence in the FASTA format\n\n");
+    fprintf(stderr, "Options: \n");
+    fprintf(stderr, "        -v        Display version information\n\n");
+    fprintf(stderr, "        -q INT    filtering reads with mapping quality less than INT [%d]\n", mapq);
+    fprintf(stderr, "        -Q INT    filtering somatic snv output with somatic quality less than  INT [%d]\n",
+            p->min_somatic_qual);
+    fprintf(stderr, "        -L FLAG   do not report LOH variants as determined by genotypes\n");
+    fprintf(stderr, "        -G FLAG   do not report Gain of Reference variants as determined by genotypes\n");
+    fprintf(stderr, "        -p FLAG   disable priors in the somatic calculation. Increases sensitivity for solid tumors\n");
+    fprintf(stderr, "        -J FLAG   Use prior probabilities accounting for the somatic mutation rate\n");
+    fprintf(stderr, "        -s FLOAT  prior probability of a somatic mutation (implies -J) [%f]\n", p->somatic_rate);
+    fprintf(stderr, "        -T FLOAT  theta in maq consensus calling model (for -c/-g) [%f]\n", p->theta);
+    fprintf(stderr, "        -N INT    number of haplotypes in the sample (for -c/-g) [%d]\n", p->n_hap);
+    fprintf(stderr, "        -r FLOAT  prior of a difference between two haplotypes (for -c/-g) [%f]\n", p->het_rate);
+    fprintf(stderr, "        -n STRING normal sample id (for VCF header) [%s]\n", "NORMAL");
+    fprintf(stderr, "        -t STRING tumor sample id (for VCF header) [%s]\n", "TUMOR");
+    fprintf(stderr, "        -F STRING select output format [%s]\n", "classic");
+    fprintf(stderr, "           Available formats:\n");
+    for (int i = 0; i < ss_format_count(); ++i) fprintf(stderr, "             %s\n", ss_format_name(i));
+    fprintf(stderr, "\n");
+}
+
+static int env_int(const char *name, int dflt)
+{
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+int main(int argc, char *argv[])
+{
+    ss_params_t prm;
+    ss_params_default(&prm);
+    const char *normal_id = "NORMAL", *tumor_id = "TUMOR", *fn_fa = NULL, *fmt_name = "classic";
+    int mapq = 0, c;
+    while ((c = getopt(argc, argv, "n:t:vf:T:N:r:I:q:Q:pLGJs:F:")) >= 0) {
+        switch (c) {
+        case 'f': fn_fa = optarg; break;
+        case 'T': prm.theta = (float)atof(optarg); break;
+        case 'N': prm.n_hap = atoi(optarg); break;
+        case 'r': prm.het_rate = (float)atof(optarg); break;
+        case 'q': mapq = atoi(optarg); break;
+        case 'Q': prm.min_somatic_qual = atoi(optarg); break;
+        case 'F': fmt_name = optarg; break;
+        case 'p': prm.use_priors = 0; break;
+        case 'J': prm.use_joint_priors = 1; break;
+        case 's': prm.somatic_rate = atof(optarg); prm.use_joint_priors = 1; break;
+        case 'v': version_info(); return 0;
+        case 't': tumor_id = optarg; break;
+        case 'n': normal_id = optarg; break;
+        case 'L': prm.include_loh = 0; break;
+        case 'G': prm.include_gor = 0; break;
+        default: fprintf(stderr, "Unrecognizd option '-%c'.\n", c); return 1;
+        }
+    }
+    if (optind == argc) { usage(argv[0], &prm, mapq); return 1; }
+    if (argc - optind < 3) {          /* the reference dereferences missing arguments */
+        usage(argv[0], &prm, mapq);
+        return 1;
+    }
+    run_t R;
+    memset(&R, 0, sizeof R);
+    R.cur_tid = -1;
+    R.pending = -1;
+    if (fn_fa) R.fai = fasta_index_load(fn_fa);
+    else {
+        fprintf(stderr, "You MUST specify a reference sequence. It isn't optional.\n");
+        exit(1);
+    }
+    if (prm.use_joint_priors)
+        fprintf(stderr, "Using priors accounting for somatic mutation rate. Prior probability of a somatic "
+                        "mutation is %f\n", prm.somatic_rate);
+    fprintf(stderr, "Preparing to snipe some somatics\n");
+    if (prm.use_priors) fprintf(stderr, "Using prior probabilities\n");
+    const int bthreads = env_int("SS_BGZF_THREADS", 4);
+    bgzf_reader_t *fp1 = bgzf_open(argv[optind], bthreads);
+    fprintf(stderr, "Normal bam is %s\n", argv[optind + 1]);
+    fprintf(stderr, "Tumor bam is %s\n", argv[optind]);
+    bam_header_t h1, h2;
+    if (!fp1 || bam_header_read(fp1, &h1)) {
+        fprintf(stderr, "[bam-somaticsniper] cannot read BAM %s\n", argv[optind]);
+        return 1;
+    }
+    bgzf_reader_t *fp2 = bgzf_open(argv[optind + 1], bthreads);
+    if (!fp2 || bam_header_read(fp2, &h2)) {
+        fprintf(stderr, "[bam-somaticsniper] cannot read BAM %s\n", argv[optind + 1]);
+        return 1;
+    }
+    R.h1 = &h1;
+    R.out = fopen(argv[optind + 2], "w");
+    const int fmt = ss_format_lookup(fmt_name);
+    if (fmt < 0) {
+        fprintf(stderr, "unknown output format: '%s'. Abort!\n", fmt_name);
+        exit(1);
+    }
+    R.fmt = fmt;
+    if (!R.out) {
+        fprintf(stderr, "Unable to open snp file!!!!!!!!!\n");
+        exit(1);
+    }
+    const char *dump = getenv("SS_DUMP_PILEUP");
+    if (dump && *dump) R.dump = fopen(dump, "w");
+    const int pileup_only = R.dump && env_int("SS_PILEUP_ONLY", 0);
+    const int rc_ctx = pileup_only ? SS_OK : ss_ctx_create(&prm, env_int("SS_DEVICE", 0), &R.ctx);
+    if (rc_ctx) {
+        fprintf(stderr, "[bam-somaticsniper] cannot create the GPU scorer: %s\n", ss_strerror(rc_ctx));
+        return 1;
+    }
+    ss_write_header(R.out, fmt, fn_fa, normal_id, tumor_id);
+    const int cap = env_int("SS_BATCH", 1 << 20);
+    batch_init(&R.bat[0], (size_t)(cap > 0 ? cap : 1 << 20));
+    batch_init(&R.bat[1], (size_t)(cap > 0 ? cap : 1 << 20));
+    pthread_mutex_init(&R.mu, NULL);
+    pthread_cond_init(&R.cv, NULL);
+    R.pileup_only = pileup_only;
+    pthread_create(&R.th, NULL, scorer_main, &R);
+    dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, on_site, &R);
+    if (R.bat[R.fill].n) submit(&R);
+    pthread_mutex_lock(&R.mu);
+    R.quit = 1;
+    pthread_cond_broadcast(&R.cv);
+    pthread_mutex_unlock(&R.mu);
+    pthread_join(R.th, NULL);
+    bgzf_close(fp1);
+    bgzf_close(fp2);
+    bam_header_free(&h1);
+    bam_header_free(&h2);
+    fasta_index_free(R.fai);
+    free(R.cur_ref);
+    batch_free(&R.bat[0]);
+    batch_free(&R.bat[1]);
+    if (R.ctx) ss_ctx_destroy(R.ctx);
+    if (R.dump) fclose(R.dump);
+    fclose(R.out);
+    return R.failed ? 1 : 0;
+}

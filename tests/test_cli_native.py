@@ -1,0 +1,135 @@
+"""The native drop-in CLI (somatic-sniper_amd/bam-somaticsniper: own BGZF/BAM
+reader, FASTA index, dual pileup and writers; GPU scoring through the C ABI)
+against the reference CLI compiled from /root/reference (oracle/_ref).
+
+CPU tests compare the site stream the two walkers hand to the scorer: the
+native SS_DUMP_PILEUP/SS_PILEUP_ONLY hook against the reference CLI whose
+glf_somatic is wrapped to dump the same fields (oracle/pileup_dump_shim.c).
+GPU tests compare the output files byte for byte for every format and option
+set, and the reference's own integration test (expected.vcf)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(ROOT, "somatic-sniper_amd", "bam-somaticsniper")
+REF_CLI = os.path.join(ROOT, "oracle", "_ref", "bam-somaticsniper")
+REF_DUMP = os.path.join(ROOT, "oracle", "_ref", "bam-somaticsniper-dump")
+ITEST = os.path.join(ROOT, "tests", "golden", "integration")
+
+need_native = pytest.mark.skipif(not os.path.exists(NATIVE), reason="native CLI not built")
+need_ref = pytest.mark.skipif(not os.path.exists(REF_CLI), reason="reference CLI not built")
+need_dump = pytest.mark.skipif(not os.path.exists(REF_DUMP), reason="reference dump CLI not built")
+
+OPTSETS = [[], ["-Q", "0"], ["-J"], ["-J", "-s", "1e-5", "-Q", "5"], ["-p", "-Q", "0"],
+           ["-L", "-G", "-Q", "0"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-q", "20", "-Q", "0"]]
+
+
+def _run(cmd, cwd, env=None):
+    return subprocess.run(cmd, cwd=cwd, capture_output=True, text=True, timeout=600,
+                          env=dict(os.environ, **(env or {})))
+
+
+@pytest.fixture(scope="module")
+def datasets(tmp_path_factory):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bamgen
+    out = []
+    d = tmp_path_factory.mktemp("itest")
+    for f in os.listdir(ITEST):
+        shutil.copy(os.path.join(ITEST, f), d)
+    out.append((str(d), "small.fa", "t-small.bam", "n-small.bam"))
+    for seed, kw in [(1, {}), (2, dict(depth_t=60, depth_n=30)), (3, dict(exotic=False, lengths=(5000,))),
+                     (4, dict(lengths=(400, 300, 900, 200, 700), depth_t=15, depth_n=12))]:
+        d = tmp_path_factory.mktemp(f"pair{seed}")
+        bamgen.make_pair(str(d), seed=seed, **kw)
+        out.append((str(d), "ref.fa", "tumor.bam", "normal.bam"))
+    return out
+
+
+def _dump(cli, d, fa, t, n, opts, native):
+    name = f"{'nat' if native else 'ref'}_{abs(hash(tuple(opts)))}.dump"
+    env = {"SS_DUMP_PILEUP": name}
+    if native:
+        env["SS_PILEUP_ONLY"] = "1"
+    p = _run([cli] + opts + ["-f", fa, t, n, "out_" + name], d, env)
+    assert p.returncode == 0, p.stderr
+    path = os.path.join(d, name)       # the reference shim only creates it at the first site
+    return open(path, "rb").read() if os.path.exists(path) else b""
+
+
+@need_native
+@need_dump
+@pytest.mark.parametrize("opts", [[], ["-q", "20"], ["-q", "61"]])
+def test_pileup_site_stream_matches_reference(datasets, opts):
+    for d, fa, t, n in datasets:
+        ref = _dump(REF_DUMP, d, fa, t, n, opts, native=False)
+        nat = _dump(NATIVE, d, fa, t, n, opts, native=True)
+        assert nat == ref, (d, opts)
+
+
+@need_native
+@need_ref
+def test_fasta_index_matches_reference(datasets, tmp_path):
+    for d, fa, *_ in datasets:
+        a, b = tmp_path / "a", tmp_path / "b"
+        a.mkdir(exist_ok=True)
+        b.mkdir(exist_ok=True)
+        shutil.copy(os.path.join(d, fa), a / fa)
+        shutil.copy(os.path.join(d, fa), b / fa)
+        _run([REF_CLI, "-f", fa, "x.bam", "y.bam", "o"], str(a))          # builds a/fa.fai, then fails on the BAMs
+        _run([NATIVE, "-f", fa, "x.bam", "y.bam", "o"], str(b), {"SS_PILEUP_ONLY": "1", "SS_DUMP_PILEUP": "d"})
+        assert (a / (fa + ".fai")).read_bytes() == (b / (fa + ".fai")).read_bytes()
+
+
+@need_native
+def test_native_cli_fails_loudly_without_gpu(datasets):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    d, fa, t, n = datasets[0]
+    p = _run([NATIVE, "-f", fa, t, n, "out.txt"], d)
+    assert p.returncode != 0 and "GPU scorer" in p.stderr
+
+
+@need_native
+def test_native_cli_usage_and_errors(tmp_path):
+    p = _run([NATIVE], str(tmp_path))
+    assert p.returncode == 1 and "-f FILE   REQUIRED reference sequence" in p.stderr
+    p = _run([NATIVE, "-I", "x"], str(tmp_path))
+    assert p.returncode == 1 and "Unrecognizd option '-I'." in p.stderr
+    p = _run([NATIVE, "-v"], str(tmp_path))
+    assert p.returncode == 0 and p.stdout.startswith("Somatic Sniper version")
+
+
+@pytest.mark.gpu
+@need_native
+def test_native_integration_expected_vcf(datasets):
+    d, fa, t, n = datasets[0]
+    p = _run([NATIVE, "-F", "vcf", "-f", fa, t, n, "native.vcf"], d)
+    assert p.returncode == 0, p.stderr
+    drop = ("##fileDate", "##reference")
+    keep = lambda s: [l for l in s.splitlines() if not l.startswith(drop)]
+    assert keep(open(os.path.join(d, "native.vcf")).read()) == keep(open(os.path.join(ITEST, "expected.vcf")).read())
+
+
+@pytest.mark.gpu
+@need_native
+@need_ref
+@pytest.mark.parametrize("fmt", ["classic", "vcf", "bed"])
+def test_native_cli_matches_reference(datasets, fmt):
+    strip = lambda s: "".join(l for l in s.splitlines(True) if not l.startswith("##fileDate"))
+    for d, fa, t, n in datasets:
+        for opts in OPTSETS:
+            args = ["-F", fmt] + opts + ["-f", fa, t, n]
+            pr = _run([REF_CLI] + args + ["ref.out"], d)
+            pn = _run([NATIVE] + args + ["nat.out"], d, {"SS_BATCH": "1000"})
+            assert pr.returncode == 0 and pn.returncode == 0, (pr.stderr, pn.stderr)
+            ref = open(os.path.join(d, "ref.out")).read()
+            nat = open(os.path.join(d, "nat.out")).read()
+            assert strip(nat) == strip(ref), (d, fmt, opts)
+            quiet = lambda e: e.replace("[fai_load] build FASTA index.\n", "")
+            assert quiet(pn.stderr) == quiet(pr.stderr), (pn.stderr, pr.stderr)
