@@ -8,8 +8,12 @@
 typedef struct pl_node {
     bam_record_t b;
     uint32_t beg, end;
+    uint32_t pk;                  /* mapQ | strand << 20 of the record */
+    const uint8_t *seq, *qual;
     struct pl_node *next;
 } pl_node_t;
+
+#define SLAB 512
 
 typedef struct {
     /* list of loaded reads; `tail` is always a spare node that receives the
@@ -26,6 +30,8 @@ typedef struct {
     bgzf_reader_t *fp;
     bam_record_t rec;          /* read buffer */
     int error;
+    pl_node_t **slabs;
+    int n_slabs, slab_used;
 } walker_t;
 
 static pl_node_t *node_new(walker_t *w)
@@ -36,9 +42,15 @@ static pl_node_t *node_new(walker_t *w)
         p->next = NULL;
         return p;
     }
-    p = (pl_node_t *)calloc(1, sizeof *p);
-    if (!p) { fprintf(stderr, "out of memory\n"); exit(1); }
-    return p;
+    if (w->slab_used == SLAB || !w->slabs) {     /* fresh nodes come from contiguous slabs */
+        pl_node_t **sl = (pl_node_t **)realloc(w->slabs, sizeof(pl_node_t *) * (size_t)(w->n_slabs + 1));
+        pl_node_t *blk = (pl_node_t *)calloc(SLAB, sizeof(pl_node_t));
+        if (!sl || !blk) { fprintf(stderr, "out of memory\n"); exit(1); }
+        w->slabs = sl;
+        w->slabs[w->n_slabs++] = blk;
+        w->slab_used = 0;
+    }
+    return &w->slabs[w->n_slabs - 1][w->slab_used++];
 }
 
 static void node_free(walker_t *w, pl_node_t *p)
@@ -52,6 +64,11 @@ static void node_free(walker_t *w, pl_node_t *p)
 static int locate(const bam_record_t *b, uint32_t pos, int32_t *qpos, uint8_t *is_del)
 {
     const uint32_t *cig = bam_rec_cigar(b);
+    if (b->n_cigar == 1 && (cig[0] & 0xf) == SS_CIG_M && pos - (uint32_t)b->pos < (cig[0] >> 4)) {
+        *qpos = (int32_t)(pos - (uint32_t)b->pos);        /* a plain match: the common case */
+        *is_del = 0;
+        return 1;
+    }
     uint32_t x = (uint32_t)b->pos, y = 0;
     int keep = 1;
     *qpos = -1;
@@ -96,11 +113,12 @@ static void walker_init(walker_t *w, bgzf_reader_t *fp, int mask, int thresh)
 
 static void walker_free(walker_t *w)
 {
-    pl_node_t *p = w->head;
-    while (p) { pl_node_t *q = p->next; bam_record_free(&p->b); free(p); p = q; }
-    if (w->spare) { bam_record_free(&w->spare->b); free(w->spare); }
-    p = w->free_list;
-    while (p) { pl_node_t *q = p->next; bam_record_free(&p->b); free(p); p = q; }
+    for (int i = 0; i < w->n_slabs; ++i) {
+        const int n = i == w->n_slabs - 1 ? w->slab_used : SLAB;
+        for (int k = 0; k < n; ++k) bam_record_free(&w->slabs[i][k].b);
+        free(w->slabs[i]);
+    }
+    free(w->slabs);
     bam_record_free(&w->rec);
     free(w->pu);
 }
@@ -132,8 +150,12 @@ static int next_pos(walker_t *w)
                     }
                     pl_entry_t *e = &w->pu[n];
                     e->b = &p->b;
-                    if (!(p->b.flag & SS_BAM_FUNMAP) && locate(&p->b, (uint32_t)w->pos, &e->qpos, &e->is_del))
+                    if (!(p->b.flag & SS_BAM_FUNMAP) && locate(&p->b, (uint32_t)w->pos, &e->qpos, &e->is_del)) {
+                        const int q = e->qpos;
+                        e->packed = p->pk | (uint32_t)p->qual[q] << 8 |
+                                    (uint32_t)((p->seq[q >> 1] >> ((~q & 1) << 2)) & 0xf) << 16;
                         ++n;
+                    }
                 }
             }
             w->head = w->spare->next;
@@ -146,6 +168,9 @@ static int next_pos(walker_t *w)
                 bam_record_copy(&w->tail->b, &w->rec);
                 w->tail->beg = (uint32_t)w->rec.pos;
                 w->tail->end = bam_rec_end(&w->rec);
+                w->tail->pk = (uint32_t)w->rec.mapq | ((w->rec.flag & SS_BAM_FREVERSE) ? 1u << 20 : 0u);
+                w->tail->seq = bam_rec_seq(&w->tail->b);
+                w->tail->qual = bam_rec_qual(&w->tail->b);
                 if (w->rec.tid < w->max_tid) {
                     fprintf(stderr, "[bam_pileup_core] the input is not sorted. Abort!\n");
                     abort();

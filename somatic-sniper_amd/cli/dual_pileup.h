@@ -21,6 +21,7 @@ typedef struct {
     const bam_record_t *b;
     int32_t qpos;
     uint8_t is_del;
+    uint32_t packed;      /* SS_READ_PACK of this entry (valid when !is_del) */
 } pl_entry_t;
 
 /* Called for every reported position; return non-zero to stop the walk. */

@@ -20,9 +20,9 @@
  * Environment: SS_DEVICE (GPU index, default 0), SS_BATCH (sites per batch,
  * default 2^20), SS_BGZF_THREADS (inflate threads per BAM, default 4),
  * SS_DUMP_PILEUP=FILE (test hook: also write every reported site, see
- * dump_site()), SS_PILEUP_ONLY=1 (test hook with SS_DUMP_PILEUP: walk and dump
- * without scoring, so the pileup restatement is testable on a host without a
- * GPU; no output records are written).
+ * dump_site()), SS_PILEUP_ONLY=1 (test / timing hook: walk (and dump) without
+ * scoring, so the pileup restatement is testable on a host without a GPU; no
+ * output records are written).
  */
 #include <getopt.h>
 #include <pthread.h>
@@ -204,8 +204,7 @@ static void pack(batch_t *b, const pl_entry_t *pu, int n, int tumor)
     for (int i = 0; i < n; ++i) {
         const pl_entry_t *e = &pu[i];
         if (e->is_del || (e->b->flag & SS_BAM_FUNMAP)) continue;
-        o[k++] = SS_READ_PACK(e->b->mapq, bam_rec_qual(e->b)[e->qpos], bam_rec_base(e->b, e->qpos),
-                              (e->b->flag & SS_BAM_FREVERSE) ? 1u : 0u);
+        o[k++] = e->packed;
     }
     *len += k;
 }
@@ -361,7 +360,7 @@ int main(int argc, char *argv[])
     }
     const char *dump = getenv("SS_DUMP_PILEUP");
     if (dump && *dump) R.dump = fopen(dump, "w");
-    const int pileup_only = R.dump && env_int("SS_PILEUP_ONLY", 0);
+    const int pileup_only = env_int("SS_PILEUP_ONLY", 0);
     const int rc_ctx = pileup_only ? SS_OK : ss_ctx_create(&prm, env_int("SS_DEVICE", 0), &R.ctx);
     if (rc_ctx) {
         fprintf(stderr, "[bam-somaticsniper] cannot create the GPU scorer: %s\n", ss_strerror(rc_ctx));
