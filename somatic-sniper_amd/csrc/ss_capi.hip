@@ -28,7 +28,7 @@ struct ss_ctx {
     /* model on the device */
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
-    uint32_t *d_counters;     /* [0] deep, [1] giant, [2] err, [3] scratch n_calls, [4] clamped */
+    uint32_t *d_counters;     /* [0] deep, [1] giant, [2] err, [3] scratch n_calls, [4] clamped, [5] deep2 */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
     uint32_t *d_giant_list;
@@ -180,6 +180,8 @@ extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double
     return SS_OK;
 }
 
+/* the deep list buffer holds two lists of deep_cap entries: the main
+ * kernel's (deep) and the wide kernel's overflow (deep2) */
 static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites)
 {
     if (n_sites <= c->deep_cap) return SS_OK;
@@ -191,7 +193,7 @@ static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites)
         c->d_deep_list = nullptr;
     }
     c->deep_cap = 0;
-    if (dev_alloc((void **)&c->d_deep_list, cap * sizeof(uint32_t))) return SS_E_NOMEM;
+    if (dev_alloc((void **)&c->d_deep_list, 2 * cap * sizeof(uint32_t))) return SS_E_NOMEM;
     c->deep_cap = (uint32_t)cap;
     return SS_OK;
 }
@@ -210,6 +212,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     hipStream_t s = (hipStream_t)stream;
     /* counters: deep, giant, (err is sticky), scratch n_calls, scratch clamped */
     HIPCHK(hipMemsetAsync(c->d_counters, 0, 2 * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
     memset(&a, 0, sizeof(a));
@@ -228,6 +231,8 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.deep_list = c->d_deep_list;
     a.deep_count = c->d_counters + 0;
     a.deep_cap = c->deep_cap;
+    a.deep2_list = c->d_deep_list + c->deep_cap;
+    a.deep2_count = c->d_counters + 5;
     a.giant_list = c->d_giant_list;
     a.giant_count = c->d_counters + 1;
     a.giant_cap = c->giant_cap;
@@ -267,7 +272,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         e1 = (*c->ev)[2 * c->n_logged + 1];
         ++c->n_logged;
     }
-    int e = ss_launch_score(a, (int)blocks, deep_grid, s, e0, e1);
+    int e = ss_launch_score(a, (int)blocks, c->n_cu, deep_grid, s, e0, e1);
     return e == 0 ? SS_OK : SS_E_HIP;
 }
 

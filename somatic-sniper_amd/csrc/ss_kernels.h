@@ -65,6 +65,8 @@ struct ss_score_args {
     uint32_t  *deep_list;     /* sites with a sample deeper than the main-kernel limit */
     uint32_t  *deep_count;
     uint32_t   deep_cap;
+    uint32_t  *deep2_list;    /* sites too deep for the wide kernel (ss_score_wide) */
+    uint32_t  *deep2_count;
     uint32_t  *giant_list;    /* sites deeper than the LDS limit of the deep kernel */
     uint32_t  *giant_count;
     uint32_t   giant_cap;
@@ -85,9 +87,11 @@ struct ss_score_args {
 #define SS_DEEP_BLOCK      256
 #define SS_DEEP_MAXN       4096  /* per-sample depth sorted in LDS by the deep kernel */
 #define SS_GIANT_BLOCKS    8
+#define SS_WIDE_BLOCK      256   /* 4 waves, one workgroup per CU (LDS)          */
+#define SS_WIDE_MAXSLOTS   2048  /* sort slots (tumor + pad + normal) per site    */
 
 /* Launchers (return hipError_t as int). */
-int ss_launch_score(const ss_score_args &a, int main_grid, int deep_grid, hipStream_t s,
+int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, hipStream_t s,
                     hipEvent_t ev0, hipEvent_t ev1);
 int ss_launch_synth_depth(const ss_synth_k_t &k, uint64_t first, uint64_t n, uint8_t *ref,
                           uint32_t *dt, uint32_t *dn, hipStream_t s);

@@ -596,6 +596,26 @@ __device__ __forceinline__ uint32_t key_to_rec(uint32_t k)
     return q | 1u << 16 | st << 28;
 }
 
+/* 16-bit fold record (wide kernel, whose LDS arena holds 16 deep sites):
+ *   bits 0..7 q | bit 12 strand | bit 13 1 (fsum multiplier);
+ * (r >> 8) & 31 is strand << 4 like the u32 record's top byte. */
+__device__ __forceinline__ uint32_t key_to_rec16(uint32_t k)
+{
+    const uint32_t minq = (k >> 5) & 0xffu, st = (k >> 3) & 1u, nz = k & 1u;
+    const uint32_t q = (minq < 4u && nz) ? 4u : minq;
+    return q | st << 12 | 1u << 13;
+}
+
+template <typename RecT> struct RecForm;
+template <> struct RecForm<uint32_t> {
+    static __device__ __forceinline__ uint32_t shift(uint32_t r) { return r >> 24; }
+    static constexpr uint32_t ONE_BIT = 16u;
+};
+template <> struct RecForm<uint16_t> {
+    static __device__ __forceinline__ uint32_t shift(uint32_t r) { return (r >> 8) & 31u; }
+    static constexpr uint32_t ONE_BIT = 13u;
+};
+
 __device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b)
 {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -836,6 +856,9 @@ __device__ __forceinline__ void packed_bitonic_flip(uint32_t (&v)[M][K])
     flip_stage<M, K, 128>(v);
     if constexpr (K >= 2) flip_stage<M, K, 256>(v);
     if constexpr (K >= 4) flip_stage<M, K, 512>(v);
+    if constexpr (K >= 8) flip_stage<M, K, 1024>(v);
+    if constexpr (K >= 16) flip_stage<M, K, 2048>(v);
+    static_assert(K == 1 || K == 2 || K == 4 || K == 8 || K == 16, "sort size");
 }
 
 /* number of u16 keys (both halves of all K registers) below x, wave-wide */
@@ -951,11 +974,12 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
  * record's strand<<4 field and saturated at w = 255 (:170).  Base groups are
  * walked longest first, so the wave-wide trip count is set by one long chain
  * per lane. */
-__device__ __forceinline__ void fold_sample(const uint32_t *rec, const uint32_t cnt[4],
+template <typename RecT>
+__device__ __forceinline__ void fold_sample(const RecT *rec, const uint32_t cnt[4],
                                             const double *fk, uint32_t role, float acc[4])
 {
     const uint32_t start1 = cnt[0], start2 = cnt[0] + cnt[1], start3 = start2 + cnt[2];
-    const uint32_t moff = role ? 16u : 0u, mwid = role ? 1u : 8u;
+    const uint32_t moff = role ? RecForm<RecT>::ONE_BIT : 0u, mwid = role ? 1u : 8u;
     const char *fkb = reinterpret_cast<const char *>(fk);
     uint32_t L = 0;
 #pragma unroll
@@ -967,15 +991,15 @@ __device__ __forceinline__ void fold_sample(const uint32_t *rec, const uint32_t 
         const uint32_t b = i == 0 ? L : (i - 1u) + ((i - 1u) >= L ? 1u : 0u);
         const uint32_t s0 = b == 0 ? 0u : (b == 1 ? start1 : (b == 2 ? start2 : start3));
         const uint32_t t = b == 0 ? cnt[0] : (b == 1 ? cnt[1] : (b == 2 ? cnt[2] : cnt[3]));
-        const uint32_t *p0 = rec + s0;
-        const uint32_t *p = p0 + t;
+        const RecT *p0 = rec + s0;
+        const RecT *p = p0 + t;
         float e = 0.0f;
         uint32_t W = 0;
 #pragma unroll 2
         while (p != p0) {
             --p;
             const uint32_t r = *p;
-            const uint32_t sh = r >> 24;                 /* 0 or 16 */
+            const uint32_t sh = RecForm<RecT>::shift(r);  /* 0 or 16 */
             uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
             w8 = w8 < 2040u ? w8 : 2040u;
             W += 8u << sh;
@@ -1015,11 +1039,26 @@ __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s
 #define D_REF(i) rl(desc, 17u + (i))
 #define D_N(i) rl(desc, 33u + (i))
 
-__device__ __forceinline__ void push_deep(const ss_score_args &a, uint32_t site)
+/* Hand every site of the block (descriptor `desc`) that needs more sort
+ * slots than the packed main-kernel sort (PK_MAX, incl. the pad element) to
+ * the wide kernel: one atomic per block, not per site. */
+__device__ __forceinline__ void push_block_deep(const ss_score_args &a, uint32_t desc, uint32_t nsite,
+                                                uint64_t sblk)
 {
-    if (lane_id() == 0) {
-        const uint32_t d = atomicAdd(a.deep_count, 1u);
-        if (d < a.deep_cap) a.deep_list[d] = site;
+    const uint32_t lane = lane_id();
+    const int i = (int)(lane & 15u);
+    const uint32_t t0 = (uint32_t)__shfl((int)desc, i), t1 = (uint32_t)__shfl((int)desc, i + 1);
+    const uint32_t n0 = (uint32_t)__shfl((int)desc, 33 + i), n1 = (uint32_t)__shfl((int)desc, 34 + i);
+    const uint32_t nt = t1 - t0;
+    const bool deep = lane < nsite && (nt + (nt & 1u) + (n1 - n0)) > PK_MAX;
+    const uint64_t mask = __ballot(deep);
+    if (mask == 0) return;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(a.deep_count, (uint32_t)__popcll(mask));
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    if (deep) {
+        const uint32_t d = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        if (d < a.deep_cap) a.deep_list[d] = (uint32_t)(sblk + lane);
         else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
     }
 }
@@ -1040,7 +1079,7 @@ __device__ __forceinline__ Sub form_sub(const ss_score_args &a, uint32_t desc, u
         const uint32_t ntl = D_T(i + 1u) - D_T(i);
         const uint32_t sz = ntl + (D_N(i + 1u) - D_N(i));
         if (sz + (ntl & 1u) > PK_MAX) {        /* sort slots incl. the pad element */
-            if (i == pos) { push_deep(a, (uint32_t)(sblk + i)); pos = ++i; continue; }
+            if (i == pos) { pos = ++i; continue; }     /* listed by push_block_deep */
             break;
         }
         if (tot + sz > STG) break;
@@ -1070,8 +1109,10 @@ __device__ __forceinline__ void issue_dma(const ss_score_args &a, const Sub &r, 
                                              (lds_void_t *)(buf + r.lt + i), 4, 0, 0);
 }
 
-/* Phases B, C, D for the G sites of a sub-group. */
-__device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32_t *stage,
+/* Phases B, C, D for the G sites of a sub-group.  Fold records are RecT
+ * entries of `recs` (slot rec_n index); `stage` only receives the next DMA. */
+template <typename RecT>
+__device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const RecT *recs, uint32_t *stage,
                                            const Slot3 *slot, SlotRes *res, const uint32_t *sites,
                                            const uint32_t *refcs, const double *fk,
                                            bool have_next, const Sub &nxt, uint32_t diag)
@@ -1088,8 +1129,8 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
         cnt[2] = m3.cnt23 & 0xffffu; cnt[3] = m3.cnt23 >> 16;
         depth = m3.rec_n >> 16;
         rms = m3.rms;
-        const uint32_t *rec = stage + (m3.rec_n & 0xffffu);
-        if (!(diag & 2u)) fold_sample(rec, cnt, fk, role, acc);
+        const RecT *rec = recs + (m3.rec_n & 0xffffu);
+        if (!(diag & 2u)) fold_sample<RecT>(rec, cnt, fk, role, acc);
         else {
 #pragma unroll
             for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b];
@@ -1165,7 +1206,8 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, uint32
 /* DIAG = true only for the profiling ablations (SS_DIAG); the production
  * instance has every ablation branch folded away. */
 template <bool DIAG>
-__global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
+__global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
+void ss_score_main(ss_score_args a)
 {
     const uint32_t diag = DIAG ? a.diag : 0u;
     __shared__ double fk[256];
@@ -1189,6 +1231,7 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
     uint32_t nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
     uint64_t nblk = blk + nwaves;
     uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
+    push_block_deep(a, desc, nsite, blk * GB);
     Sub cur = form_sub(a, desc, nsite, 0, blk * GB);
     while (cur.a == cur.b) {               /* whole block deep */
         blk = nblk;
@@ -1197,6 +1240,7 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
         nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
         nblk = blk + nwaves;
         ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
+        push_block_deep(a, desc, nsite, blk * GB);
         cur = form_sub(a, desc, nsite, 0, blk * GB);
     }
     issue_dma(a, cur, stage);
@@ -1252,13 +1296,153 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) void ss_score_main(ss_score_args a)
             nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
             nblk = blk + nwaves;
             ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
+            push_block_deep(a, desc, nsite, blk * GB);
             nxt = form_sub(a, desc, nsite, 0, blk * GB);
             have = nxt.a < nxt.b;
         }
         /* ---- phases B + C + D (the next DMA is issued after the fold) ---- */
-        finish_sub(a, G, stage, slot, res, sites, refcs, fk, have, nxt, diag);
+        finish_sub<uint32_t>(a, G, stage, stage, slot, res, sites, refcs, fk, have, nxt, diag);
         if (!have) break;
         cur = nxt;
+    }
+}
+
+/* --------------------------------------------------------------------------
+ * Wide kernel: the sites the main kernel left on the deep list (more than
+ * PK_MAX sort slots, e.g. 500x/500x panels), up to SS_WIDE_MAXSLOTS slots.
+ *
+ * One workgroup per CU, four independent waves; each wave owns a 36 KB LDS
+ * arena of 16-bit fold records.  A wave takes 16 list entries at a time and,
+ * site by site, loads the packed reads straight from HBM into registers,
+ * sorts them with the same packed bitonic network as the main kernel
+ * (1024 or 2048 slots: K = 8 or 16 registers), and writes the fold records
+ * of both samples contiguously into the arena.  Then the sites are folded
+ * together -- lane = (site, sample, role), so the wave runs up to 64 serial
+ * chains at once instead of one -- and finished by the main kernel's code.
+ * Sites beyond SS_WIDE_MAXSLOTS go to the second deep list (ss_score_deep).
+ * ------------------------------------------------------------------------ */
+namespace {
+
+#define WIDE_ARENA 18432    /* u16 records per wave (16 sites x ~1150) */
+
+struct WideLds {
+    uint16_t arena[4][WIDE_ARENA];
+    Slot3    slot[4][2 * GB];
+    SlotRes  res[4][2 * GB];
+    uint32_t site[4][GB];
+    uint32_t refc[4][GB];
+};
+
+template <int K>
+__device__ __forceinline__ void sort_site_wide(const ss_score_args &a, uint32_t ot, uint32_t nt, uint32_t on,
+                                               uint32_t nn, uint32_t ref16, uint32_t cap, uint16_t *arena,
+                                               uint32_t base, Slot3 *st2)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t ntr = nt + (nt & 1u);
+    uint32_t tb, th;
+    nt_tables(ref16, tb, th);
+    uint32_t v[1][K];
+    uint32_t a_t = 0, a_n = 0;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
+        const bool tum = e0 < ntr;
+        const uint32_t *src = tum ? a.reads_t + ot + e0 : a.reads_n + on + (e0 - ntr);
+        const uint32_t lim = tum ? nt : ntr + nn;
+        const bool in0 = e0 < lim, in1 = e0 + 1u < lim;
+        const uint32_t rd0 = in0 ? src[0] : 0u, rd1 = in1 ? src[1] : 0u;   /* 0 = no contribution */
+        const uint32_t sb = tum ? 0u : 0x8000u;
+        const uint32_t k0 = read_key16(rd0, tb, th, sb), k1 = read_key16(rd1, tb, th, sb);
+        const uint32_t t0 = min(rd0 & 0x7fu, cap), t1 = min(rd1 & 0x7fu, cap);
+        const uint32_t x = t0 * t0 + t1 * t1;
+        a_t += tum ? x : 0u;
+        a_n += tum ? 0u : x;
+        v[0][r] = k0 | k1 << 16;
+    }
+    packed_bitonic_flip<1, K>(v);
+    const uint32_t c1 = count_below<K>(v[0], 1u << 13), c2 = count_below<K>(v[0], 2u << 13);
+    const uint32_t c3 = count_below<K>(v[0], 3u << 13), c4 = count_below<K>(v[0], 4u << 13);
+    const uint32_t c5 = count_below<K>(v[0], 5u << 13), c6 = count_below<K>(v[0], 6u << 13);
+    const uint32_t c7 = count_below<K>(v[0], 7u << 13), c8 = count_below<K>(v[0], 0xffffu);
+    /* sorted order is [tumor groups][normal groups]: records are contiguous */
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
+            if (e < c8) arena[base + e] = (uint16_t)key_to_rec16((v[0][r] >> (16 * h)) & 0xffffu);
+        }
+    const uint32_t rms_t = wave_sum(a_t), rms_n = wave_sum(a_n);
+    if (lane == 0) {
+        st2[0].rec_n = base | nt << 16;
+        st2[0].cnt01 = c1 | (c2 - c1) << 16;
+        st2[0].cnt23 = (c3 - c2) | (c4 - c3) << 16;
+        st2[0].rms = rms_t;
+        st2[1].rec_n = (base + c4) | nn << 16;
+        st2[1].cnt01 = (c5 - c4) | (c6 - c5) << 16;
+        st2[1].cnt23 = (c7 - c6) | (c8 - c7) << 16;
+        st2[1].rms = rms_n;
+    }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
+{
+    __shared__ double fk[256];
+    __shared__ WideLds L;
+    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = threadIdx.x >> 6;
+    uint16_t *arena = L.arena[wv];
+    Slot3 *slot = L.slot[wv];
+    SlotRes *res = L.res[wv];
+    uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
+    const uint32_t cap = (uint32_t)a.m.cap_mapQ;
+    const uint32_t count = *a.deep_count < a.deep_cap ? *a.deep_count : a.deep_cap;
+    const uint32_t ngroups = (count + GB - 1) / GB;
+    const Sub none = {0, 0, 0, 0, 0, 0};
+    for (uint32_t g = blockIdx.x * (SS_WIDE_BLOCK / 64) + wv; g < ngroups;
+         g += gridDim.x * (SS_WIDE_BLOCK / 64)) {
+        const uint32_t first = g * GB, nlist = count - first < GB ? count - first : GB;
+        uint32_t i = 0;
+        while (i < nlist) {
+            int G = 0;
+            uint32_t used = 0;
+            while (i < nlist) {
+                const uint32_t s = a.deep_list[first + i];
+                const uint32_t ot = a.off_t[s], nt = a.off_t[s + 1] - ot;
+                const uint32_t on = a.off_n[s], nn = a.off_n[s + 1] - on;
+                const uint32_t slots = nt + (nt & 1u) + nn;
+                if (slots > SS_WIDE_MAXSLOTS) {
+                    if (lane == 0) {
+                        const uint32_t d = atomicAdd(a.deep2_count, 1u);
+                        if (d < a.deep_cap) a.deep2_list[d] = s;
+                        else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
+                    }
+                    ++i;
+                    continue;
+                }
+                if (used + slots > WIDE_ARENA) break;
+                const uint32_t refc = a.ref[s];
+                const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
+                if (slots <= 1024u)
+                    sort_site_wide<8>(a, ot, nt, on, nn, ref16, cap, arena, used, slot + 2 * G);
+                else
+                    sort_site_wide<16>(a, ot, nt, on, nn, ref16, cap, arena, used, slot + 2 * G);
+                if (lane == 0) {
+                    sites[G] = s;
+                    refcs[G] = refc;
+                }
+                used += slots;
+                ++G;
+                ++i;
+            }
+            wave_sync();
+            if (G) finish_sub<uint16_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, 0u);
+        }
     }
 }
 
@@ -1339,10 +1523,10 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
     __shared__ uint32_t lbuf[GIANT ? 1 : 2][GIANT ? 1 : SS_DEEP_MAXN];
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
-    const uint32_t count = GIANT ? *a.giant_count : *a.deep_count;
+    const uint32_t count = GIANT ? *a.giant_count : *a.deep2_count;
     const uint32_t lim = GIANT ? (count < a.giant_cap ? count : a.giant_cap)
                                : (count < a.deep_cap ? count : a.deep_cap);
-    const uint32_t *list = GIANT ? a.giant_list : a.deep_list;
+    const uint32_t *list = GIANT ? a.giant_list : a.deep2_list;
     uint32_t *bt, *bn;
     if (GIANT) {
         bt = a.giant_scratch + (size_t)blockIdx.x * 2u * a.giant_keys;
@@ -1422,7 +1606,7 @@ __global__ void ss_synth_reads_kernel(ss_synth_k_t k, uint64_t first, uint64_t n
 /* --------------------------------------------------------------------------
  * launchers
  * ------------------------------------------------------------------------ */
-int ss_launch_score(const ss_score_args &a, int main_grid, int deep_grid, hipStream_t s,
+int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, hipStream_t s,
                     hipEvent_t ev0, hipEvent_t ev1)
 {
     hipError_t e;
@@ -1431,6 +1615,8 @@ int ss_launch_score(const ss_score_args &a, int main_grid, int deep_grid, hipStr
     else hipLaunchKernelGGL(ss_score_main<false>, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev1) (void)hipEventRecord(ev1, s);
+    hipLaunchKernelGGL(ss_score_wide, dim3(wide_grid), dim3(SS_WIDE_BLOCK), 0, s, a);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(ss_score_deep<false>, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(ss_score_deep<true>, dim3(SS_GIANT_BLOCKS), dim3(SS_DEEP_BLOCK), 0, s, a);
