@@ -174,7 +174,7 @@ _LIB = None
 
 
 def library_path() -> str:
-    return os.environ.get("SNIPER_AMD_LIB", os.path.join(_HERE, "libsniper_amd.so"))
+    return os.environ.get("SNIPER_AMD_LIB") or os.path.join(_HERE, "libsniper_amd.so")
 
 
 def load_library():

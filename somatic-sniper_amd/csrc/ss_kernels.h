@@ -87,7 +87,9 @@ struct ss_score_args {
 #define SS_DEEP_BLOCK      256
 #define SS_DEEP_MAXN       4096  /* per-sample depth sorted in LDS by the deep kernel */
 #define SS_GIANT_BLOCKS    8
-#define SS_WIDE_BLOCK      256   /* 4 waves, one workgroup per CU (LDS)          */
+#ifndef SS_WIDE_BLOCK
+#define SS_WIDE_BLOCK      512   /* 8 waves, one workgroup per CU (LDS)          */
+#endif
 #define SS_WIDE_MAXSLOTS   2048  /* sort slots (tumor + pad + normal) per site    */
 
 /* Launchers (return hipError_t as int). */

@@ -1311,8 +1311,8 @@ void ss_score_main(ss_score_args a)
  * Wide kernel: the sites the main kernel left on the deep list (more than
  * PK_MAX sort slots, e.g. 500x/500x panels), up to SS_WIDE_MAXSLOTS slots.
  *
- * One workgroup per CU, four independent waves; each wave owns a 36 KB LDS
- * arena of 16-bit fold records.  A wave takes 16 list entries at a time and,
+ * One workgroup per CU, SS_WIDE_BLOCK / 64 independent waves sharing 144 KB
+ * of LDS as per-wave arenas of 16-bit fold records.  A wave takes 16 list entries at a time and,
  * site by site, loads the packed reads straight from HBM into registers,
  * sorts them with the same packed bitonic network as the main kernel
  * (1024 or 2048 slots: K = 8 or 16 registers), and writes the fold records
@@ -1323,23 +1323,46 @@ void ss_score_main(ss_score_args a)
  * ------------------------------------------------------------------------ */
 namespace {
 
-#define WIDE_ARENA 18432    /* u16 records per wave (16 sites x ~1150) */
+#define WIDE_WAVES (SS_WIDE_BLOCK / 64)
+#define WIDE_ARENA (73728 / WIDE_WAVES)   /* u16 records per wave: 144 KB of LDS in all */
 
 struct WideLds {
-    uint16_t arena[4][WIDE_ARENA];
-    Slot3    slot[4][2 * GB];
-    SlotRes  res[4][2 * GB];
-    uint32_t site[4][GB];
-    uint32_t refc[4][GB];
+    uint16_t arena[WIDE_WAVES][WIDE_ARENA];
+    Slot3    slot[WIDE_WAVES][2 * GB];
+    SlotRes  res[WIDE_WAVES][2 * GB];
+    uint32_t site[WIDE_WAVES][GB];
+    uint32_t refc[WIDE_WAVES][GB];
 };
 
-template <int K>
-__device__ __forceinline__ void sort_site_wide(const ss_score_args &a, uint32_t ot, uint32_t nt, uint32_t on,
-                                               uint32_t nn, uint32_t ref16, uint32_t cap, uint16_t *arena,
-                                               uint32_t base, Slot3 *st2)
+/* A wide site's packed reads in the sort placement (tumor [0, nt), normal
+ * [ntr, ntr + nn)): element pair (e0, e0 + 1), e0 = 2 * (r * 64 + lane), in
+ * rd[2r], rd[2r + 1]; 0 (no contribution) outside the site.  Issued one site
+ * ahead of its sort so the HBM latency overlaps the previous site's work. */
+struct WideSite {
+    uint32_t ot, nt, on, nn;
+};
+
+__device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite &w, uint32_t (&rd)[32])
 {
     const uint32_t lane = lane_id();
-    const uint32_t ntr = nt + (nt & 1u);
+    const uint32_t ntr = w.nt + (w.nt & 1u);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
+        const bool tum = e0 < ntr;
+        const uint32_t *src = tum ? a.reads_t + w.ot + e0 : a.reads_n + w.on + (e0 - ntr);
+        const uint32_t lim = tum ? w.nt : ntr + w.nn;
+        rd[2 * r] = e0 < lim ? __builtin_nontemporal_load(src) : 0u;
+        rd[2 * r + 1] = e0 + 1u < lim ? __builtin_nontemporal_load(src + 1) : 0u;
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void sort_site_wide(const uint32_t (&rd)[32], const WideSite &w, uint32_t ref16,
+                                               uint32_t cap, uint16_t *arena, uint32_t base, Slot3 *st2)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t nt = w.nt, nn = w.nn, ntr = nt + (nt & 1u);
     uint32_t tb, th;
     nt_tables(ref16, tb, th);
     uint32_t v[1][K];
@@ -1348,10 +1371,7 @@ __device__ __forceinline__ void sort_site_wide(const ss_score_args &a, uint32_t 
     for (int r = 0; r < K; ++r) {
         const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
         const bool tum = e0 < ntr;
-        const uint32_t *src = tum ? a.reads_t + ot + e0 : a.reads_n + on + (e0 - ntr);
-        const uint32_t lim = tum ? nt : ntr + nn;
-        const bool in0 = e0 < lim, in1 = e0 + 1u < lim;
-        const uint32_t rd0 = in0 ? src[0] : 0u, rd1 = in1 ? src[1] : 0u;   /* 0 = no contribution */
+        const uint32_t rd0 = rd[2 * r], rd1 = rd[2 * r + 1];
         const uint32_t sb = tum ? 0u : 0x8000u;
         const uint32_t k0 = read_key16(rd0, tb, th, sb), k1 = read_key16(rd1, tb, th, sb);
         const uint32_t t0 = min(rd0 & 0x7fu, cap), t1 = min(rd1 & 0x7fu, cap);
@@ -1407,38 +1427,57 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
     for (uint32_t g = blockIdx.x * (SS_WIDE_BLOCK / 64) + wv; g < ngroups;
          g += gridDim.x * (SS_WIDE_BLOCK / 64)) {
         const uint32_t first = g * GB, nlist = count - first < GB ? count - first : GB;
-        uint32_t i = 0;
+        /* site i's reads are in flight while site i-1 is sorted */
+        uint32_t i = 0, s_cur = 0;
+        WideSite w_cur = {0, 0, 0, 0};
+        uint32_t rd[32];
+        auto describe = [&](uint32_t k, uint32_t &s, WideSite &w) {
+            s = a.deep_list[first + k];
+            w.ot = a.off_t[s];
+            w.nt = a.off_t[s + 1] - w.ot;
+            w.on = a.off_n[s];
+            w.nn = a.off_n[s + 1] - w.on;
+        };
+        if (nlist) {
+            describe(0, s_cur, w_cur);
+            wide_load(a, w_cur, rd);
+        }
         while (i < nlist) {
             int G = 0;
             uint32_t used = 0;
             while (i < nlist) {
-                const uint32_t s = a.deep_list[first + i];
-                const uint32_t ot = a.off_t[s], nt = a.off_t[s + 1] - ot;
-                const uint32_t on = a.off_n[s], nn = a.off_n[s + 1] - on;
-                const uint32_t slots = nt + (nt & 1u) + nn;
+                const uint32_t s = s_cur;
+                const WideSite w = w_cur;
+                const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
+                if (used + slots > WIDE_ARENA && slots <= SS_WIDE_MAXSLOTS) break;   /* next sub-group */
+                uint32_t cur[32];
+#pragma unroll
+                for (int k = 0; k < 32; ++k) cur[k] = rd[k];
+                if (i + 1 < nlist) {
+                    describe(i + 1, s_cur, w_cur);
+                    wide_load(a, w_cur, rd);
+                }
+                ++i;
                 if (slots > SS_WIDE_MAXSLOTS) {
                     if (lane == 0) {
                         const uint32_t d = atomicAdd(a.deep2_count, 1u);
                         if (d < a.deep_cap) a.deep2_list[d] = s;
                         else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
                     }
-                    ++i;
                     continue;
                 }
-                if (used + slots > WIDE_ARENA) break;
                 const uint32_t refc = a.ref[s];
                 const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
                 if (slots <= 1024u)
-                    sort_site_wide<8>(a, ot, nt, on, nn, ref16, cap, arena, used, slot + 2 * G);
+                    sort_site_wide<8>(cur, w, ref16, cap, arena, used, slot + 2 * G);
                 else
-                    sort_site_wide<16>(a, ot, nt, on, nn, ref16, cap, arena, used, slot + 2 * G);
+                    sort_site_wide<16>(cur, w, ref16, cap, arena, used, slot + 2 * G);
                 if (lane == 0) {
                     sites[G] = s;
                     refcs[G] = refc;
                 }
                 used += slots;
                 ++G;
-                ++i;
             }
             wave_sync();
             if (G) finish_sub<uint16_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, 0u);
