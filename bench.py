@@ -32,6 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# BASELINE.json "metric", verbatim
+METRIC = "pileup sites/sec at 60\u00d7T/30\u00d7N; 1\u21928 GPU scaling; achieved HBM GB/s vs roofline"
 
 
 def cpu_baseline(lt, ln, sample, seed, gpu_scores_prefix):
@@ -164,7 +166,7 @@ def main():
             traffic = None
 
     result = {
-        "metric": "pileup sites/sec at 60xT/30xN (1->8 GPU scaling; achieved HBM GB/s vs roofline)",
+        "metric": METRIC,
         "value": round(total_sites / elapsed, 1),
         "unit": "sites/s",
         "n_gpus": world,
@@ -198,6 +200,8 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
     if world > 1:
         dist.destroy_process_group()
 
