@@ -1268,8 +1268,9 @@ void ss_score_main(ss_score_args a)
                     refcs[G + m] = rdesc & 0xffu;
                 }
             }
-            if (i + 1u < cur.b && tot[0] <= 128u && tot[1] <= 128u) {
-                sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, diag);   /* two sites, interleaved */
+            if (i + 1u < cur.b && tot[0] <= 256u && tot[1] <= 256u) {   /* two sites, interleaved */
+                if (tot[0] <= 128u && tot[1] <= 128u) sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, diag);
+                else sort_sites<2, 2>(stage, S2, cap, slot + 2 * G, diag);
                 G += 2;
                 i += 2;
                 continue;
