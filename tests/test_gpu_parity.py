@@ -74,6 +74,23 @@ def test_deep_parity(pkg, oracle, ctx, lt, ln, fixed, n):
     assert_parity(pkg, oracle, batch, ctx=ctx)
 
 
+def test_kernel_routing_mix(pkg, oracle, ctx):
+    """One batch whose sites take every route: main kernel (<= 512 sort slots),
+    wide kernel (<= 2048), deep kernel via the wide kernel's overflow list
+    (<= 4096 per sample), and the giant kernel, interleaved so each kernel sees
+    non-contiguous site indices."""
+    parts = [pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=1, **EXOTIC), 7 * k, n)
+             for k, (lt, ln, n) in enumerate([(60, 30, 40), (600, 500, 12), (1500, 1200, 6), (4200, 300, 3),
+                                              (30, 2, 40), (900, 900, 6)])]
+    sites = []
+    for i in range(40):
+        for b in parts:
+            if i < b.n_sites:
+                sites.append(b.site(i))
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), ctx=ctx)
+    ctx.check()
+
+
 def test_giant_parity(pkg, oracle, ctx):
     """> 4096 reads in a sample -> giant kernel with global scratch."""
     big = pkg.synth_batch_host(pkg.Synth.default(6000, 4500, fixed_depth=1, **EXOTIC), 0, 6)
