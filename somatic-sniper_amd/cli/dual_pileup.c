@@ -6,23 +6,31 @@
 #include <string.h>
 
 typedef struct pl_node {
-    bam_record_t b;
+    /* hot fields first: read on every visited position */
+    int32_t tid;
     uint32_t beg, end;
     uint32_t pk;                  /* mapQ | strand << 20 of the record */
     const uint8_t *seq, *qual;
-    struct pl_node *next;
+    uint32_t span;                /* length of the single M operation, or 0 */
+    struct pl_node *next;         /* free-list link */
+    bam_record_t b;
 } pl_node_t;
 
 #define SLAB 512
 
 typedef struct {
-    /* list of loaded reads; `tail` is always a spare node that receives the
-     * next record, so an empty list has head == tail, and head->b is then the
-     * last record that passed the filters (whether it was kept or not) */
-    pl_node_t *head, *tail, *spare;
+    /* Loaded reads in load order (the reference's linked list, kept here as
+     * an array that is compacted in order).  `tail` is the spare node that
+     * receives the next record: with no loaded reads the reference's list
+     * head IS that spare node, whose record is then the last one copied into
+     * it -- or, for a node recycled from the pool, whatever it held before
+     * (the pool is LIFO like samtools' mempool, so this is reproduced). */
+    pl_node_t **act;
+    int n_act, m_act;
+    pl_node_t *tail;
     pl_node_t *free_list;
     int32_t tid, pos, max_tid, max_pos;
-    int is_eof, started;
+    int is_eof;
     uint32_t flag_mask;
     int mapq_thresh;
     pl_entry_t *pu;
@@ -104,8 +112,8 @@ static void walker_init(walker_t *w, bgzf_reader_t *fp, int mask, int thresh)
 {
     memset(w, 0, sizeof *w);
     w->fp = fp;
-    w->head = w->tail = node_new(w);
-    w->spare = node_new(w);
+    w->tail = node_new(w);
+    (void)node_new(w);        /* the reference's dummy node: keeps pool allocation in step */
     w->max_tid = w->max_pos = -1;
     w->flag_mask = mask < 0 ? SS_BAM_DEF_MASK : (SS_BAM_FUNMAP | (uint32_t)mask);
     w->mapq_thresh = thresh < 0 ? 0 : thresh;
@@ -119,6 +127,7 @@ static void walker_free(walker_t *w)
         free(w->slabs[i]);
     }
     free(w->slabs);
+    free(w->act);
     bam_record_free(&w->rec);
     free(w->pu);
 }
@@ -128,58 +137,75 @@ static void walker_free(walker_t *w)
 static int next_pos(walker_t *w)
 {
     if (w->max_pos != -1) {
-        if (w->tid < w->head->b.tid) { w->tid = w->head->b.tid; w->pos = 0; }
+        const pl_node_t *head = w->n_act ? w->act[0] : w->tail;
+        if (w->tid < head->tid) { w->tid = head->tid; w->pos = 0; }
         else ++w->pos;
     }
-    if (w->is_eof && w->head->next == NULL) return -1;
+    if (w->is_eof && w->n_act == 0) return -1;
     for (;;) {
         if (w->is_eof || w->max_tid > w->tid || (w->max_tid == w->tid && w->max_pos > w->pos)) {
-            int n = 0;
-            pl_node_t *q = w->spare;           /* stands in front of head */
-            q->next = w->head;
-            for (pl_node_t *p = w->head; p->next; q = p, p = p->next) {
-                if (p->b.tid < w->tid || (p->b.tid == w->tid && p->end <= (uint32_t)w->pos)) {
-                    q->next = p->next;
-                    node_free(w, p);
-                    p = q;
-                } else if (p->b.tid == w->tid && p->beg <= (uint32_t)w->pos) {
-                    if (n == w->max_pu) {
-                        w->max_pu = w->max_pu ? w->max_pu << 1 : 256;
-                        w->pu = (pl_entry_t *)realloc(w->pu, sizeof(pl_entry_t) * (size_t)w->max_pu);
-                        if (!w->pu) { fprintf(stderr, "out of memory\n"); exit(1); }
-                    }
-                    pl_entry_t *e = &w->pu[n];
-                    e->b = &p->b;
-                    if (!(p->b.flag & SS_BAM_FUNMAP) && locate(&p->b, (uint32_t)w->pos, &e->qpos, &e->is_del)) {
-                        const int q = e->qpos;
-                        e->packed = p->pk | (uint32_t)p->qual[q] << 8 |
-                                    (uint32_t)((p->seq[q >> 1] >> ((~q & 1) << 2)) & 0xf) << 16;
-                        ++n;
-                    }
-                }
+            if (w->n_act > w->max_pu) {
+                w->max_pu = w->n_act + 256;
+                w->pu = (pl_entry_t *)realloc(w->pu, sizeof(pl_entry_t) * (size_t)w->max_pu);
+                if (!w->pu) { fprintf(stderr, "out of memory\n"); exit(1); }
             }
-            w->head = w->spare->next;
-            w->spare->next = NULL;
+            const int32_t tid = w->tid;
+            const uint32_t pos = (uint32_t)w->pos;
+            int n = 0, k = 0;
+            for (int i = 0; i < w->n_act; ++i) {
+                pl_node_t *p = w->act[i];
+                if (p->tid < tid || (p->tid == tid && p->end <= pos)) {   /* passed: back to the pool */
+                    node_free(w, p);
+                    continue;
+                }
+                w->act[k++] = p;
+                if (p->tid != tid || p->beg > pos) continue;
+                pl_entry_t *e = &w->pu[n];
+                e->b = &p->b;
+                const uint32_t off = pos - p->beg;
+                if (off < p->span) {                    /* a plain match: the common case */
+                    e->qpos = (int32_t)off;
+                    e->is_del = 0;
+                } else if (!locate(&p->b, pos, &e->qpos, &e->is_del)) {
+                    continue;                           /* inside a reference skip */
+                }
+                if (!e->is_del) {
+                    const int q = e->qpos;
+                    e->packed = p->pk | (uint32_t)p->qual[q] << 8 |
+                                (uint32_t)((p->seq[q >> 1] >> ((~q & 1) << 2)) & 0xf) << 16;
+                }
+                ++n;
+            }
+            w->n_act = k;
             return n;
         }
         const int rc = bam_record_read(w->fp, &w->rec);
         if (rc > 0) {
             if (!(w->rec.flag & w->flag_mask) && !(w->rec.mapq < w->mapq_thresh)) {
-                bam_record_copy(&w->tail->b, &w->rec);
-                w->tail->beg = (uint32_t)w->rec.pos;
-                w->tail->end = bam_rec_end(&w->rec);
-                w->tail->pk = (uint32_t)w->rec.mapq | ((w->rec.flag & SS_BAM_FREVERSE) ? 1u << 20 : 0u);
-                w->tail->seq = bam_rec_seq(&w->tail->b);
-                w->tail->qual = bam_rec_qual(&w->tail->b);
+                pl_node_t *t = w->tail;
+                bam_record_copy(&t->b, &w->rec);
+                t->tid = w->rec.tid;
+                t->beg = (uint32_t)w->rec.pos;
+                t->end = bam_rec_end(&w->rec);
+                t->pk = (uint32_t)w->rec.mapq | ((w->rec.flag & SS_BAM_FREVERSE) ? 1u << 20 : 0u);
+                t->seq = bam_rec_seq(&t->b);
+                t->qual = bam_rec_qual(&t->b);
+                t->span = (t->b.n_cigar == 1 && (bam_rec_cigar(&t->b)[0] & 0xf) == SS_CIG_M)
+                              ? bam_rec_cigar(&t->b)[0] >> 4 : 0u;
                 if (w->rec.tid < w->max_tid) {
                     fprintf(stderr, "[bam_pileup_core] the input is not sorted. Abort!\n");
                     abort();
                 }
                 w->max_tid = w->rec.tid;
-                w->max_pos = (int32_t)w->tail->beg;
-                if (w->tail->end > (uint32_t)w->pos) {
-                    w->tail->next = node_new(w);
-                    w->tail = w->tail->next;
+                w->max_pos = (int32_t)t->beg;
+                if (t->end > (uint32_t)w->pos) {            /* kept: it joins the loaded reads */
+                    if (w->n_act == w->m_act) {
+                        w->m_act = w->m_act ? 2 * w->m_act : 256;
+                        w->act = (pl_node_t **)realloc(w->act, sizeof(pl_node_t *) * (size_t)w->m_act);
+                        if (!w->act) { fprintf(stderr, "out of memory\n"); exit(1); }
+                    }
+                    w->act[w->n_act++] = t;
+                    w->tail = node_new(w);
                 }
             }
         } else {
