@@ -1,6 +1,7 @@
 /* dual_pileup.c -- see dual_pileup.h for the behaviour being reproduced. */
 #include "dual_pileup.h"
 
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -215,28 +216,180 @@ static int next_pos(walker_t *w)
     }
 }
 
-int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, dual_site_fn fn,
-                    void *data)
+/* packed non-deleted reads of the current position's entries */
+static int packed_of(const walker_t *w, int n, uint32_t *dst)
+{
+    int k = 0;
+    for (int i = 0; i < n; ++i)
+        if (!w->pu[i].is_del) dst[k++] = w->pu[i].packed;
+    return k;
+}
+
+/* ---- threaded mode: each walk produces a stream of steps -------------------
+ * One step per next_pos call: {tid, pos, r, np} + np packed reads.  Steps go
+ * to the consumer in chunks through a small ring (single producer, single
+ * consumer).  A walk runs ahead of the lockstep loop by at most the ring. */
+#define CHUNK_STEPS 4096
+#define N_CHUNKS 8
+
+typedef struct {
+    int32_t *hdr;            /* 4 ints per step */
+    uint32_t *pk;
+    size_t n_steps, n_pk, cap_pk;
+} chunk_t;
+
+typedef struct {
+    walker_t *w;
+    chunk_t chunks[N_CHUNKS];
+    uint64_t produced, consumed;     /* chunk counters */
+    int stop;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    pthread_t th;
+    /* consumer cursor */
+    chunk_t *cur;
+    size_t step, pk_off;
+    int ended;                       /* the walk returned -1: it keeps returning -1 */
+} stream_t;
+
+static void *walk_main(void *arg)
+{
+    stream_t *S = (stream_t *)arg;
+    walker_t *w = S->w;
+    uint32_t *tmp = NULL;
+    int m_tmp = 0;
+    for (int done = 0; !done;) {
+        pthread_mutex_lock(&S->mu);
+        while (!S->stop && S->produced - S->consumed >= N_CHUNKS) pthread_cond_wait(&S->cv, &S->mu);
+        const int stop = S->stop;
+        pthread_mutex_unlock(&S->mu);
+        if (stop) break;
+        chunk_t *c = &S->chunks[S->produced % N_CHUNKS];
+        c->n_steps = c->n_pk = 0;
+        while (c->n_steps < CHUNK_STEPS) {
+            const int r = next_pos(w);
+            int np = 0;
+            if (r > 0) {
+                if (r > m_tmp) { m_tmp = r + 256; tmp = (uint32_t *)realloc(tmp, 4 * (size_t)m_tmp); }
+                np = packed_of(w, r, tmp);
+                if (c->n_pk + (size_t)np > c->cap_pk) {
+                    c->cap_pk = 2 * (c->n_pk + (size_t)np) + 4096;
+                    c->pk = (uint32_t *)realloc(c->pk, 4 * c->cap_pk);
+                    if (!c->pk) { fprintf(stderr, "out of memory\n"); exit(1); }
+                }
+                memcpy(c->pk + c->n_pk, tmp, 4 * (size_t)np);
+                c->n_pk += (size_t)np;
+            }
+            int32_t *h = c->hdr + 4 * c->n_steps++;
+            h[0] = w->tid; h[1] = w->pos; h[2] = r; h[3] = np;
+            if (r < 0) { done = 1; break; }
+        }
+        pthread_mutex_lock(&S->mu);
+        ++S->produced;
+        pthread_cond_broadcast(&S->cv);
+        pthread_mutex_unlock(&S->mu);
+    }
+    free(tmp);
+    return NULL;
+}
+
+/* next step of a stream: returns r and sets tid/pos/packed view */
+static int stream_next(stream_t *S, int32_t *tid, int32_t *pos, const uint32_t **pk, int *np)
+{
+    if (S->ended) { *np = 0; return -1; }    /* next_pos after the end returns -1 again */
+    if (!S->cur || S->step == S->cur->n_steps) {
+        pthread_mutex_lock(&S->mu);
+        if (S->cur) { ++S->consumed; pthread_cond_broadcast(&S->cv); }
+        while (S->produced == S->consumed) pthread_cond_wait(&S->cv, &S->mu);
+        S->cur = &S->chunks[S->consumed % N_CHUNKS];
+        pthread_mutex_unlock(&S->mu);
+        S->step = 0;
+        S->pk_off = 0;
+    }
+    const int32_t *h = S->cur->hdr + 4 * S->step++;
+    *tid = h[0]; *pos = h[1]; *np = h[3];
+    *pk = S->cur->pk + S->pk_off;
+    S->pk_off += (size_t)h[3];
+    if (h[2] < 0) S->ended = 1;
+    return h[2];
+}
+
+int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, int threaded,
+                    dual_site_fn fn, void *data)
 {
     walker_t *w1 = (walker_t *)malloc(sizeof(walker_t)), *w2 = (walker_t *)malloc(sizeof(walker_t));
     if (!w1 || !w2) { free(w1); free(w2); return -1; }
     walker_init(w1, fp1, mask, thresh);
     walker_init(w2, fp2, mask, thresh);
     int r1 = -1, r2 = -1, stop = 0;
-    while (!stop && (r1 = next_pos(w1)) >= 0 && (r2 = next_pos(w2)) >= 0) {
-        do {
-            if (w2->tid > w1->tid)
-                while (w2->tid > w1->tid && (r1 = next_pos(w1)) >= 0) {}
-            if (w1->tid > w2->tid)
-                while (w2->tid < w1->tid && (r2 = next_pos(w2)) >= 0) {}
-        } while (w2->tid != w1->tid && r1 >= 0 && r2 >= 0);
-        if (r1 > 0 && r2 > 0) {
-            if (w1->tid != w2->tid || w1->pos != w2->pos) {
-                fprintf(stderr, "[dual_pileup] tumor and normal walks out of step. Abort!\n");
-                abort();
+    if (!threaded) {
+        uint32_t *pk1 = NULL, *pk2 = NULL;
+        int m1 = 0, m2 = 0;
+        while (!stop && (r1 = next_pos(w1)) >= 0 && (r2 = next_pos(w2)) >= 0) {
+            do {
+                if (w2->tid > w1->tid)
+                    while (w2->tid > w1->tid && (r1 = next_pos(w1)) >= 0) {}
+                if (w1->tid > w2->tid)
+                    while (w2->tid < w1->tid && (r2 = next_pos(w2)) >= 0) {}
+            } while (w2->tid != w1->tid && r1 >= 0 && r2 >= 0);
+            if (r1 > 0 && r2 > 0) {
+                if (w1->tid != w2->tid || w1->pos != w2->pos) {
+                    fprintf(stderr, "[dual_pileup] tumor and normal walks out of step. Abort!\n");
+                    abort();
+                }
+                if (r1 > m1) { m1 = r1 + 256; pk1 = (uint32_t *)realloc(pk1, 4 * (size_t)m1); }
+                if (r2 > m2) { m2 = r2 + 256; pk2 = (uint32_t *)realloc(pk2, 4 * (size_t)m2); }
+                const int np1 = packed_of(w1, r1, pk1), np2 = packed_of(w2, r2, pk2);
+                stop = fn(w1->tid, w1->pos, r1, r2, pk1, np1, pk2, np2, data);
             }
-            stop = fn(w1->tid, w1->pos, r1, r2, w1->pu, w2->pu, data);
         }
+        free(pk1);
+        free(pk2);
+    } else {
+        stream_t *S = (stream_t *)calloc(2, sizeof(stream_t));
+        if (!S) return -1;
+        for (int k = 0; k < 2; ++k) {
+            S[k].w = k ? w2 : w1;
+            for (int c = 0; c < N_CHUNKS; ++c) {
+                S[k].chunks[c].hdr = (int32_t *)malloc(sizeof(int32_t) * 4 * CHUNK_STEPS);
+                if (!S[k].chunks[c].hdr) { fprintf(stderr, "out of memory\n"); exit(1); }
+            }
+            pthread_mutex_init(&S[k].mu, NULL);
+            pthread_cond_init(&S[k].cv, NULL);
+            pthread_create(&S[k].th, NULL, walk_main, &S[k]);
+        }
+        int32_t t1 = 0, p1 = 0, t2 = 0, p2 = 0;
+        const uint32_t *pk1 = NULL, *pk2 = NULL;
+        int np1 = 0, np2 = 0;
+        while (!stop && (r1 = stream_next(&S[0], &t1, &p1, &pk1, &np1)) >= 0 &&
+               (r2 = stream_next(&S[1], &t2, &p2, &pk2, &np2)) >= 0) {
+            do {
+                if (t2 > t1)
+                    while (t2 > t1 && (r1 = stream_next(&S[0], &t1, &p1, &pk1, &np1)) >= 0) {}
+                if (t1 > t2)
+                    while (t2 < t1 && (r2 = stream_next(&S[1], &t2, &p2, &pk2, &np2)) >= 0) {}
+            } while (t2 != t1 && r1 >= 0 && r2 >= 0);
+            if (r1 > 0 && r2 > 0) {
+                if (t1 != t2 || p1 != p2) {
+                    fprintf(stderr, "[dual_pileup] tumor and normal walks out of step. Abort!\n");
+                    abort();
+                }
+                stop = fn(t1, p1, r1, r2, pk1, np1, pk2, np2, data);
+            }
+        }
+        for (int k = 0; k < 2; ++k) {
+            pthread_mutex_lock(&S[k].mu);
+            S[k].stop = 1;
+            if (S[k].cur) ++S[k].consumed;
+            S[k].consumed = S[k].produced;      /* release every chunk: the walk may be waiting */
+            pthread_cond_broadcast(&S[k].cv);
+            pthread_mutex_unlock(&S[k].mu);
+            pthread_join(S[k].th, NULL);
+            for (int c = 0; c < N_CHUNKS; ++c) { free(S[k].chunks[c].hdr); free(S[k].chunks[c].pk); }
+            pthread_mutex_destroy(&S[k].mu);
+            pthread_cond_destroy(&S[k].cv);
+        }
+        free(S);
     }
     const int err = w1->error || w2->error;
     if (err) fprintf(stderr, "[dual_pileup] truncated or malformed BAM record\n");

@@ -24,14 +24,18 @@ typedef struct {
     uint32_t packed;      /* SS_READ_PACK of this entry (valid when !is_del) */
 } pl_entry_t;
 
-/* Called for every reported position; return non-zero to stop the walk. */
-typedef int (*dual_site_fn)(int32_t tid, int32_t pos, int n1, int n2, const pl_entry_t *pu1,
-                            const pl_entry_t *pu2, void *data);
+/* Called for every reported position with the raw entry counts n1 / n2
+ * (deletions included) and the packed non-deleted reads (SS_READ_PACK) of
+ * each sample in pileup order; return non-zero to stop the walk. */
+typedef int (*dual_site_fn)(int32_t tid, int32_t pos, int n1, int n2, const uint32_t *pk1, int np1,
+                            const uint32_t *pk2, int np2, void *data);
 
 /* mask < 0 selects SS_BAM_DEF_MASK, otherwise SS_BAM_FUNMAP | mask
- * (bam_plbuf_set_mask :148-152); thresh < 0 is 0.  Returns 0, or -1 on a read
+ * (bam_plbuf_set_mask :148-152); thresh < 0 is 0.  threaded != 0 runs each
+ * sample's walk on its own thread (the two walks only meet in the lockstep
+ * loop, so the reported sites are the same).  Returns 0, or -1 on a read
  * error (message on stderr). */
-int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, dual_site_fn fn,
-                    void *data);
+int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, int threaded,
+                    dual_site_fn fn, void *data);
 
 #endif

@@ -19,6 +19,7 @@
  *
  * Environment: SS_DEVICE (GPU index, default 0), SS_BATCH (sites per batch,
  * default 2^20), SS_BGZF_THREADS (inflate threads per BAM, default 4),
+ * SS_PILEUP_THREADS (1: tumor and normal walks on their own threads, 0: one thread),
  * SS_DUMP_PILEUP=FILE (test hook: also write every reported site, see
  * dump_site()), SS_PILEUP_ONLY=1 (test / timing hook: walk (and dump) without
  * scoring, so the pileup restatement is testable on a host without a GPU; no
@@ -189,24 +190,18 @@ static void submit(run_t *R)
     pthread_mutex_unlock(&R->mu);
 }
 
-static void pack(batch_t *b, const pl_entry_t *pu, int n, int tumor)
+static void pack(batch_t *b, const uint32_t *pk, int np, int tumor)
 {
     uint32_t **dst = tumor ? &b->reads_t : &b->reads_n;
     size_t *len = tumor ? &b->nt : &b->nn, *cap = tumor ? &b->capt : &b->capn;
-    if (*len + (size_t)n > *cap) {
+    if (*len + (size_t)np > *cap) {
         size_t c = *cap ? *cap : 1 << 20;
-        while (c < *len + (size_t)n) c *= 2;
+        while (c < *len + (size_t)np) c *= 2;
         *dst = (uint32_t *)xrealloc(*dst, c * 4);
         *cap = c;
     }
-    uint32_t *o = *dst + *len;
-    size_t k = 0;
-    for (int i = 0; i < n; ++i) {
-        const pl_entry_t *e = &pu[i];
-        if (e->is_del || (e->b->flag & SS_BAM_FUNMAP)) continue;
-        o[k++] = e->packed;
-    }
-    *len += k;
+    memcpy(*dst + *len, pk, 4 * (size_t)np);
+    *len += (size_t)np;
 }
 
 /* test hook: tid pos n1 n2 refchar | tumor packed reads | normal packed reads */
@@ -219,8 +214,8 @@ static void dump_site(run_t *R, const batch_t *b, size_t s, int n1, int n2)
     fputc('\n', R->dump);
 }
 
-static int on_site(int32_t tid, int32_t pos, int n1, int n2, const pl_entry_t *pu1, const pl_entry_t *pu2,
-                   void *data)
+static int on_site(int32_t tid, int32_t pos, int n1, int n2, const uint32_t *pk1, int np1,
+                   const uint32_t *pk2, int np2, void *data)
 {
     run_t *R = (run_t *)data;
     if (R->fai && tid != R->cur_tid) {          /* contig cache (somatic_sniper.c:112-117) */
@@ -233,8 +228,8 @@ static int on_site(int32_t tid, int32_t pos, int n1, int n2, const pl_entry_t *p
     b->ref[s] = (uint8_t)((R->cur_ref && pos < R->cur_len) ? R->cur_ref[pos] : 'N');
     b->tid[s] = (uint32_t)tid;
     b->pos[s] = (uint32_t)pos;
-    pack(b, pu1, n1, 1);
-    pack(b, pu2, n2, 0);
+    pack(b, pk1, np1, 1);
+    pack(b, pk2, np2, 0);
     b->off_t[s + 1] = (uint32_t)b->nt;
     b->off_n[s + 1] = (uint32_t)b->nn;
     b->n = s + 1;
@@ -374,7 +369,7 @@ int main(int argc, char *argv[])
     pthread_cond_init(&R.cv, NULL);
     R.pileup_only = pileup_only;
     pthread_create(&R.th, NULL, scorer_main, &R);
-    dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, on_site, &R);
+    dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, env_int("SS_PILEUP_THREADS", 1), on_site, &R);
     if (R.bat[R.fill].n) submit(&R);
     pthread_mutex_lock(&R.mu);
     R.quit = 1;

@@ -50,11 +50,12 @@ def datasets(tmp_path_factory):
     return out
 
 
-def _dump(cli, d, fa, t, n, opts, native):
+def _dump(cli, d, fa, t, n, opts, native, threads="1"):
     name = f"{'nat' if native else 'ref'}_{abs(hash(tuple(opts)))}.dump"
     env = {"SS_DUMP_PILEUP": name}
     if native:
         env["SS_PILEUP_ONLY"] = "1"
+        env["SS_PILEUP_THREADS"] = threads
     p = _run([cli] + opts + ["-f", fa, t, n, "out_" + name], d, env)
     assert p.returncode == 0, p.stderr
     path = os.path.join(d, name)       # the reference shim only creates it at the first site
@@ -64,10 +65,12 @@ def _dump(cli, d, fa, t, n, opts, native):
 @need_native
 @need_dump
 @pytest.mark.parametrize("opts", [[], ["-q", "20"], ["-q", "61"]])
-def test_pileup_site_stream_matches_reference(datasets, opts):
+@pytest.mark.parametrize("threads", ["1", "0"])
+def test_pileup_site_stream_matches_reference(datasets, opts, threads):
+    """threads: the tumor and normal walks on their own threads, or both on one."""
     for d, fa, t, n in datasets:
         ref = _dump(REF_DUMP, d, fa, t, n, opts, native=False)
-        nat = _dump(NATIVE, d, fa, t, n, opts, native=True)
+        nat = _dump(NATIVE, d, fa, t, n, opts, native=True, threads=threads)
         assert nat == ref, (d, opts)
 
 
