@@ -17,7 +17,7 @@ timeout -k 10 900 "$R/oracle/_ref/bam-somaticsniper" -f ref.fa tumor.bam normal.
 t2=$(date +%s.%N)
 timeout -k 10 600 "$R/somatic-sniper_amd/bam-somaticsniper" -f ref.fa tumor.bam normal.bam nat.out 2> nat.err
 t3=$(date +%s.%N)
-SS_DUMP_PILEUP=/dev/null SS_PILEUP_ONLY=1 timeout -k 10 600 "$R/somatic-sniper_amd/bam-somaticsniper" -f ref.fa tumor.bam normal.bam po.out 2>/dev/null
+SS_PILEUP_ONLY=1 timeout -k 10 600 "$R/somatic-sniper_amd/bam-somaticsniper" -f ref.fa tumor.bam normal.bam po.out 2>/dev/null
 t4=$(date +%s.%N)
 cmp ref.out nat.out && same=true || same=false
 sites=$(( LEN ))
