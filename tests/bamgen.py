@@ -72,7 +72,7 @@ def write_bam(path, contigs, records):
     for n, s in contigs:
         nb = n.encode() + b"\0"
         hdr += struct.pack("<i", len(nb)) + nb + struct.pack("<i", len(s))
-    recs = sorted(records, key=lambda r: (r[0], r[1]))
+    recs = sorted(records, key=lambda r: (r[0] if r[0] >= 0 else 1 << 30, r[1]))   # unmapped (tid -1) last
     data = hdr + b"".join(encode_record(*r) for r in recs)
     with open(path, "wb") as f:
         f.write(bgzf_blocks(data))
@@ -87,8 +87,14 @@ def write_fasta(path, contigs, width=60):
 
 
 def make_pair(outdir, seed=1, lengths=(3000, 2200, 1500, 800), depth_t=30, depth_n=24,
-              read_len=(40, 100), exotic=True):
-    """Returns paths (fasta, tumor_bam, normal_bam)."""
+              read_len=(40, 100), exotic=True, names=None, empty_normal=False, unmapped=False):
+    """Returns paths (fasta, tumor_bam, normal_bam).
+
+    names: contig names (default chr1..); the reference looks them up in the
+    FASTA index with fai_fetch's region parser, so ':' and ',' in a name
+    matter.  empty_normal: a normal BAM with a header and no reads.
+    unmapped: add flag-0x4 reads, placed next to a mate and at the tail
+    (tid -1), to both samples."""
     rng = np.random.default_rng(seed)
     contigs = []
     for ci, L in enumerate(lengths):
@@ -101,7 +107,7 @@ def make_pair(outdir, seed=1, lengths=(3000, 2200, 1500, 800), depth_t=30, depth
                 s[i] = s[i].lower()
             for i in rng.choice(L, 3, replace=False):
                 s[i] = str(rng.choice(list("MRWSYKn")))
-        contigs.append((f"chr{ci + 1}", "".join(s)))
+        contigs.append((names[ci] if names else f"chr{ci + 1}", "".join(s)))
     # variants: germline (both samples) and somatic (tumor only)
     variants = {}
     for ci, (_, s) in enumerate(contigs):
@@ -183,6 +189,14 @@ def make_pair(outdir, seed=1, lengths=(3000, 2200, 1500, 800), depth_t=30, depth
                     flag |= 0x200
                 recs.append((ci, st, f"{sample}{k}", mq, flag, cigar, "".join(seq), [int(x) for x in q]))
                 k += 1
+                if unmapped and rng.random() < 0.03:       # unmapped mate placed at this read
+                    useq = "".join(rng.choice(list("ACGT"), 50))
+                    recs.append((ci, st, f"{sample}{k}u", 0, 0x4 | 0x1, [], useq, [30] * 50))
+                    k += 1
+        if unmapped:
+            for j in range(25):
+                useq = "".join(rng.choice(list("ACGTN"), 60))
+                recs.append((-1, -1, f"{sample}un{j}", 0, 0x4, [], useq, [20] * 60))
         return recs
 
     import os
@@ -191,7 +205,7 @@ def make_pair(outdir, seed=1, lengths=(3000, 2200, 1500, 800), depth_t=30, depth
     nb = os.path.join(outdir, "normal.bam")
     write_fasta(fa, contigs)
     write_bam(tb, contigs, reads_for("t", depth_t))
-    write_bam(nb, contigs, reads_for("n", depth_n))
+    write_bam(nb, contigs, [] if empty_normal else reads_for("n", depth_n))
     return fa, tb, nb
 
 
