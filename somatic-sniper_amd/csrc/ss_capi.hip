@@ -28,9 +28,10 @@ struct ss_ctx {
     /* model on the device */
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
-    uint32_t *d_counters;     /* [0] deep, [1] giant, [2] err, [3] scratch n_calls, [4] clamped, [5] deep2 */
+    uint32_t *d_counters;     /* [0] unused, [1] giant, [2] err, [3] scratch n_calls, [4] clamped, [5] deep2 */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
+    uint32_t *d_deep_seg;     /* per-main-wave deep segment lengths [n_cu * 16 * 4] */
     uint32_t *d_giant_list;
     uint32_t giant_cap;
     uint32_t *d_giant_scratch;
@@ -91,7 +92,7 @@ extern "C" void ss_ctx_destroy(ss_ctx_t *c)
     if (!c) return;
     hipSetDevice(c->device);
     hipDeviceSynchronize();
-    void *ptrs[] = {c->d_tab, c->d_counters, c->d_deep_list, c->d_giant_list, c->d_giant_scratch, c->d_stage,
+    void *ptrs[] = {c->d_tab, c->d_counters, c->d_deep_list, c->d_deep_seg, c->d_giant_list, c->d_giant_scratch, c->d_stage,
                     c->d_cdf, c->d_scan_tmp, c->d_depth_tmp};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -140,6 +141,7 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
             }
     }
     TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t)));
+    TRY(dev_alloc((void **)&c->d_deep_seg, (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t)));
     c->giant_cap = 1u << 16;
     TRY(dev_alloc((void **)&c->d_giant_list, c->giant_cap * sizeof(uint32_t)));
     c->giant_keys = 1u << 20;
@@ -181,7 +183,7 @@ extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double
 }
 
 /* the deep list buffer holds two lists of deep_cap entries: the main
- * kernel's (deep) and the wide kernel's overflow (deep2) */
+ * kernel's per-wave segments (deep) and the wide kernel's overflow (deep2) */
 static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites)
 {
     if (n_sites <= c->deep_cap) return SS_OK;
@@ -207,10 +209,20 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         return SS_E_INVAL;
     if (o->calls && !o->n_calls) return SS_E_INVAL;
     HIPCHK(hipSetDevice(c->device));
-    int rc = ensure_deep_cap(c, b->n_sites);
+    /* main kernel: 4 waves per workgroup, one 16-site block per wave per
+     * iteration, grid-strided; 4 workgroups fit a CU (LDS), so 16 per CU gives
+     * each CU four rounds of waves for load balance.  Each wave owns a deep-list
+     * segment as long as the most blocks it can visit, times 16 sites. */
+    const uint64_t site_blocks = (b->n_sites + 15) / 16;
+    uint64_t blocks = (site_blocks + 3) / 4;
+    const uint64_t max_blocks = (uint64_t)c->n_cu * SS_MAIN_GRID_PER_CU;
+    if (blocks > max_blocks) blocks = max_blocks;
+    const uint64_t nseg = blocks * (SS_MAIN_BLOCK / 64);
+    const uint64_t seg_cap = (site_blocks + nseg - 1) / nseg * 16;
+    int rc = ensure_deep_cap(c, nseg * seg_cap);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    /* counters: deep, giant, (err is sticky), scratch n_calls, scratch clamped */
+    /* counters: giant, (err is sticky), scratch n_calls, scratch clamped, deep2 */
     HIPCHK(hipMemsetAsync(c->d_counters, 0, 2 * sizeof(uint32_t), s));
     HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
@@ -229,7 +241,9 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.glf = o->glf;
     a.n_clamped = o->n_qadd_clamped;
     a.deep_list = c->d_deep_list;
-    a.deep_count = c->d_counters + 0;
+    a.deep_seg_n = c->d_deep_seg;
+    a.deep_seg_cap = (uint32_t)seg_cap;
+    a.deep_nseg = (uint32_t)nseg;
     a.deep_cap = c->deep_cap;
     a.deep2_list = c->d_deep_list + c->deep_cap;
     a.deep2_count = c->d_counters + 5;
@@ -252,13 +266,6 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.m.min_somatic_qual = c->hm.prm.min_somatic_qual;
     a.m.flags = (c->hm.prm.use_joint_priors ? SS_MF_JOINT : 0u) | (c->hm.prm.include_loh ? SS_MF_LOH : 0u) |
                 (c->hm.prm.include_gor ? SS_MF_GOR : 0u);
-    /* main kernel: 4 waves per workgroup, one 16-site block per wave per
-     * iteration, grid-strided; 4 workgroups fit a CU (LDS), so 16 per CU gives
-     * each CU four rounds of waves for load balance */
-    const uint64_t site_blocks = (b->n_sites + 15) / 16;
-    uint64_t blocks = (site_blocks + 3) / 4;
-    const uint64_t max_blocks = (uint64_t)c->n_cu * 16;
-    if (blocks > max_blocks) blocks = max_blocks;
     const int deep_grid = c->n_cu * 4;
     c->last_stream = s;
     hipEvent_t e0 = nullptr, e1 = nullptr;

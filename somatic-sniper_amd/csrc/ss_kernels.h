@@ -62,9 +62,12 @@ struct ss_score_args {
     ss_glf_t  *glf;
     uint32_t  *n_clamped;
     /* work lists (device; counters zeroed per launch) */
-    uint32_t  *deep_list;     /* sites with a sample deeper than the main-kernel limit */
-    uint32_t  *deep_count;
-    uint32_t   deep_cap;
+    uint32_t  *deep_list;     /* sites deeper than the main-kernel limit: one segment of
+                                 deep_seg_cap entries per main-kernel wave, no atomics */
+    uint32_t  *deep_seg_n;    /* [deep_nseg] entries each main wave wrote (every wave writes) */
+    uint32_t   deep_seg_cap;
+    uint32_t   deep_nseg;     /* = main-kernel waves */
+    uint32_t   deep_cap;      /* deep2 list capacity */
     uint32_t  *deep2_list;    /* sites too deep for the wide kernel (ss_score_wide) */
     uint32_t  *deep2_count;
     uint32_t  *giant_list;    /* sites deeper than the LDS limit of the deep kernel */
@@ -83,6 +86,7 @@ struct ss_score_args {
 
 /* Launch geometry constants shared with the host. */
 #define SS_MAIN_BLOCK      256   /* 4 waves                                    */
+#define SS_MAIN_GRID_PER_CU 16   /* main-kernel workgroups per CU at most      */
 #define SS_MAIN_MAXN       256   /* per-sample depth handled by the main kernel */
 #define SS_DEEP_BLOCK      256
 #define SS_DEEP_MAXN       4096  /* per-sample depth sorted in LDS by the deep kernel */

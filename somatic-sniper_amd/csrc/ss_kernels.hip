@@ -634,6 +634,12 @@ __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b)
 #ifndef SS_XOR_BANK
 #define SS_XOR_BANK 1
 #endif
+#ifndef SS_SPLIT_SORT
+#define SS_SPLIT_SORT 1   /* skip the top merge level when each sample fits in half */
+#endif
+#ifndef SS_SPLIT_WIDE
+#define SS_SPLIT_WIDE SS_SPLIT_SORT
+#endif
 #ifndef SS_CX_EXEC
 #define SS_CX_EXEC 0      /* exec-masked max measured slower (SALU exec writes) */
 #endif
@@ -844,21 +850,42 @@ __device__ __forceinline__ void flip_stage(uint32_t (&v)[M][K])
     half_clean<M, K, (k >> 2)>(v);
 }
 
-template <int M, int K>
-__device__ __forceinline__ void packed_bitonic_flip(uint32_t (&v)[M][K])
+/* level k of the network; the top level (k = 128K, the merge of the two
+ * halves) only when `top` (wave-uniform) */
+template <int M, int K, uint32_t k>
+__device__ __forceinline__ void flip_level(uint32_t (&v)[M][K], bool top)
 {
-    flip_stage<M, K, 2>(v);
-    flip_stage<M, K, 4>(v);
-    flip_stage<M, K, 8>(v);
-    flip_stage<M, K, 16>(v);
-    flip_stage<M, K, 32>(v);
-    flip_stage<M, K, 64>(v);
-    flip_stage<M, K, 128>(v);
-    if constexpr (K >= 2) flip_stage<M, K, 256>(v);
-    if constexpr (K >= 4) flip_stage<M, K, 512>(v);
-    if constexpr (K >= 8) flip_stage<M, K, 1024>(v);
-    if constexpr (K >= 16) flip_stage<M, K, 2048>(v);
+    if constexpr (k < 128u * K) flip_stage<M, K, k>(v);
+    else if constexpr (k == 128u * K) { if (top) flip_stage<M, K, k>(v); }
+}
+
+template <int M, int K>
+__device__ __forceinline__ void packed_bitonic_flip(uint32_t (&v)[M][K], bool top = true)
+{
     static_assert(K == 1 || K == 2 || K == 4 || K == 8 || K == 16, "sort size");
+    flip_level<M, K, 2>(v, top);
+    flip_level<M, K, 4>(v, top);
+    flip_level<M, K, 8>(v, top);
+    flip_level<M, K, 16>(v, top);
+    flip_level<M, K, 32>(v, top);
+    flip_level<M, K, 64>(v, top);
+    flip_level<M, K, 128>(v, top);
+    flip_level<M, K, 256>(v, top);
+    flip_level<M, K, 512>(v, top);
+    flip_level<M, K, 1024>(v, top);
+    flip_level<M, K, 2048>(v, top);
+}
+
+/* Split placement.  Every normal key carries the sample bit, so when each
+ * sample fits in half of the network (nt, nn <= 64K) and the normal reads go
+ * to network elements 64K.. (lanes 32..63), the levels below the top leave the
+ * array [tumor sorted, pads | normal sorted, pads]: each sample sorted in its
+ * half, and the top merge level (7 of the 28 comparator stages at K = 1) is
+ * skipped.  The normal run then starts at element 64K instead of c4. */
+template <int K>
+__device__ __forceinline__ bool split_fits(uint32_t nt, uint32_t nn)
+{
+    return nt <= 64u * K && nn <= 64u * K;
 }
 
 /* number of u16 keys (both halves of all K registers) below x, wave-wide */
@@ -888,10 +915,11 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
     const uint32_t lane = lane_id();
     uint32_t v[M][K];
     uint32_t rs_t[M], rs_n[M];
-    /* input placement: tumor reads at elements [0, nt), normal reads at
-     * [ntr, ntr + nn) with ntr = nt rounded up to even, so the two elements of
-     * a lane (e0 = 2*(r*64 + lane), e0 + 1) are adjacent reads of ONE sample
-     * and come from LDS with one ds_read2 (the pad element is invalid). */
+    /* input placement (the two elements of a lane are adjacent reads of ONE
+     * sample and come from LDS with one ds_read2; a pad element is invalid) */
+    bool split = SS_SPLIT_SORT != 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) split = split && split_fits<K>(S[m].nt, S[m].nn);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
         const uint32_t nt = S[m].nt, nn = S[m].nn, ntr = nt + (nt & 1u);
@@ -900,15 +928,21 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
         uint32_t a_t = 0, a_n = 0;
 #pragma unroll
         for (int r = 0; r < K; ++r) {
+            /* i0: index of the lane's first read within its sample.  Split:
+             * lanes 0..31 (network elements < 64K) take the tumor, 32..63 the
+             * normal.  Otherwise reads are spread over all lanes (the network
+             * is indifferent to its input order). */
             const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
-            const bool tum = e0 < ntr;
-            const uint32_t idx = e0 + (tum ? S[m].bt : S[m].bn - ntr);
-            const uint32_t lim = tum ? nt : ntr + nn;
+            const uint32_t es = ((uint32_t)r * 32u + (lane & 31u)) * 2u;
+            const bool tum = split ? lane < 32u : e0 < ntr;
+            const uint32_t i0 = split ? es : (tum ? e0 : e0 - ntr);
+            const uint32_t idx = i0 + (tum ? S[m].bt : S[m].bn);
+            const uint32_t lim = tum ? nt : nn;
             const uint32_t rd0 = stage[idx], rd1 = stage[idx + 1u];
             const uint32_t sb = tum ? 0u : 0x8000u;
             uint32_t k0 = (diag & 16u) ? ((rd0 & 0x7fffu) | sb) : read_key16(rd0, tb, th, sb);
             uint32_t k1 = (diag & 16u) ? ((rd1 & 0x7fffu) | sb) : read_key16(rd1, tb, th, sb);
-            const bool in0 = e0 < lim, in1 = e0 + 1u < lim;
+            const bool in0 = i0 < lim, in1 = i0 + 1u < lim;
             k0 = in0 ? k0 : 0xffffu;
             k1 = in1 ? k1 : 0xffffu;
             const uint32_t t0 = min(rd0 & 0x7fu, cap), t1 = min(rd1 & 0x7fu, cap);
@@ -920,7 +954,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
         rs_t[m] = a_t;
         rs_n[m] = a_n;
     }
-    if (!(diag & 1u)) packed_bitonic_flip<M, K>(v);
+    if (!(diag & 1u)) packed_bitonic_flip<M, K>(v, !split);
     uint32_t *rec = stage;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -942,8 +976,10 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             for (int h = 0; h < 2; ++h) {
                 const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
                 const uint32_t key = (v[m][r] >> (16 * h)) & 0xffffu;
-                if (e < c8 && !(diag & 64u)) {
-                    const uint32_t idx = e < c4 ? bt + e : bn + (e - c4);
+                const uint32_t nb = split ? 64u * K : c4;     /* first element of the normal run */
+                const bool tum = e < nb;
+                if (e < (tum ? c4 : nb + (c8 - c4)) && !(diag & 64u)) {
+                    const uint32_t idx = tum ? bt + e : bn + (e - nb);
                     rec[idx] = key_to_rec(key);
                 }
             }
@@ -1043,7 +1079,7 @@ __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s
  * slots than the packed main-kernel sort (PK_MAX, incl. the pad element) to
  * the wide kernel: one atomic per block, not per site. */
 __device__ __forceinline__ void push_block_deep(const ss_score_args &a, uint32_t desc, uint32_t nsite,
-                                                uint64_t sblk)
+                                                uint64_t sblk, uint32_t *seg, uint32_t &ndeep)
 {
     const uint32_t lane = lane_id();
     const int i = (int)(lane & 15u);
@@ -1053,14 +1089,12 @@ __device__ __forceinline__ void push_block_deep(const ss_score_args &a, uint32_t
     const bool deep = lane < nsite && (nt + (nt & 1u) + (n1 - n0)) > PK_MAX;
     const uint64_t mask = __ballot(deep);
     if (mask == 0) return;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(a.deep_count, (uint32_t)__popcll(mask));
-    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
     if (deep) {
-        const uint32_t d = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-        if (d < a.deep_cap) a.deep_list[d] = (uint32_t)(sblk + lane);
+        const uint32_t d = ndeep + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        if (d < a.deep_seg_cap) seg[d] = (uint32_t)(sblk + lane);
         else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
     }
+    ndeep += (uint32_t)__popcll(mask);
 }
 
 struct Sub {
@@ -1226,21 +1260,31 @@ void ss_score_main(ss_score_args a)
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
 
     uint64_t blk = (uint64_t)blockIdx.x * (SS_MAIN_BLOCK / 64) + wv;
-    if (blk >= nblocks) return;
+    /* this wave's segment of the deep list; its length is stored on every exit */
+    const uint32_t gw = (uint32_t)blk;
+    uint32_t *seg = a.deep_list + (size_t)gw * a.deep_seg_cap;
+    uint32_t ndeep = 0;
+    if (blk >= nblocks) {
+        if (lane == 0) a.deep_seg_n[gw] = 0u;
+        return;
+    }
     uint32_t desc = load_desc(a, blk * GB);
     uint32_t nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
     uint64_t nblk = blk + nwaves;
     uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-    push_block_deep(a, desc, nsite, blk * GB);
+    push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
     Sub cur = form_sub(a, desc, nsite, 0, blk * GB);
     while (cur.a == cur.b) {               /* whole block deep */
         blk = nblk;
-        if (blk >= nblocks) return;
+        if (blk >= nblocks) {
+            if (lane == 0) a.deep_seg_n[gw] = ndeep;
+            return;
+        }
         desc = ndesc;
         nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
         nblk = blk + nwaves;
         ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-        push_block_deep(a, desc, nsite, blk * GB);
+        push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
         cur = form_sub(a, desc, nsite, 0, blk * GB);
     }
     issue_dma(a, cur, stage);
@@ -1297,7 +1341,7 @@ void ss_score_main(ss_score_args a)
             nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
             nblk = blk + nwaves;
             ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-            push_block_deep(a, desc, nsite, blk * GB);
+            push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
             nxt = form_sub(a, desc, nsite, 0, blk * GB);
             have = nxt.a < nxt.b;
         }
@@ -1306,6 +1350,7 @@ void ss_score_main(ss_score_args a)
         if (!have) break;
         cur = nxt;
     }
+    if (lane == 0) a.deep_seg_n[gw] = ndeep;
 }
 
 /* --------------------------------------------------------------------------
@@ -1341,7 +1386,14 @@ struct WideLds {
  * ahead of its sort so the HBM latency overlaps the previous site's work. */
 struct WideSite {
     uint32_t ot, nt, on, nn;
+    bool split;        /* split placement (see split_fits): top level skipped */
 };
+
+__device__ __forceinline__ void wide_place(WideSite &w)
+{
+    const bool k8 = w.nt + (w.nt & 1u) + w.nn <= 1024u;      /* the network sort_site_wide picks */
+    w.split = SS_SPLIT_WIDE != 0 && (k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn));
+}
 
 __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite &w, uint32_t (&rd)[32])
 {
@@ -1349,12 +1401,14 @@ __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite
     const uint32_t ntr = w.nt + (w.nt & 1u);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
-        const bool tum = e0 < ntr;
-        const uint32_t *src = tum ? a.reads_t + w.ot + e0 : a.reads_n + w.on + (e0 - ntr);
-        const uint32_t lim = tum ? w.nt : ntr + w.nn;
-        rd[2 * r] = e0 < lim ? __builtin_nontemporal_load(src) : 0u;
-        rd[2 * r + 1] = e0 + 1u < lim ? __builtin_nontemporal_load(src + 1) : 0u;
+        const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;            /* as in sort_sites */
+        const uint32_t es = ((uint32_t)r * 32u + (lane & 31u)) * 2u;
+        const bool tum = w.split ? lane < 32u : e0 < ntr;
+        const uint32_t i0 = w.split ? es : (tum ? e0 : e0 - ntr);
+        const uint32_t *src = tum ? a.reads_t + w.ot + i0 : a.reads_n + w.on + i0;
+        const uint32_t lim = tum ? w.nt : w.nn;
+        rd[2 * r] = i0 < lim ? __builtin_nontemporal_load(src) : 0u;
+        rd[2 * r + 1] = i0 + 1u < lim ? __builtin_nontemporal_load(src + 1) : 0u;
     }
 }
 
@@ -1371,7 +1425,7 @@ __device__ __forceinline__ void sort_site_wide(const uint32_t (&rd)[32], const W
 #pragma unroll
     for (int r = 0; r < K; ++r) {
         const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
-        const bool tum = e0 < ntr;
+        const bool tum = w.split ? lane < 32u : e0 < ntr;
         const uint32_t rd0 = rd[2 * r], rd1 = rd[2 * r + 1];
         const uint32_t sb = tum ? 0u : 0x8000u;
         const uint32_t k0 = read_key16(rd0, tb, th, sb), k1 = read_key16(rd1, tb, th, sb);
@@ -1381,18 +1435,21 @@ __device__ __forceinline__ void sort_site_wide(const uint32_t (&rd)[32], const W
         a_n += tum ? 0u : x;
         v[0][r] = k0 | k1 << 16;
     }
-    packed_bitonic_flip<1, K>(v);
+    packed_bitonic_flip<1, K>(v, !w.split);
     const uint32_t c1 = count_below<K>(v[0], 1u << 13), c2 = count_below<K>(v[0], 2u << 13);
     const uint32_t c3 = count_below<K>(v[0], 3u << 13), c4 = count_below<K>(v[0], 4u << 13);
     const uint32_t c5 = count_below<K>(v[0], 5u << 13), c6 = count_below<K>(v[0], 6u << 13);
     const uint32_t c7 = count_below<K>(v[0], 7u << 13), c8 = count_below<K>(v[0], 0xffffu);
-    /* sorted order is [tumor groups][normal groups]: records are contiguous */
+    /* records of both samples are written contiguously: [tumor groups][normal groups] */
+    const uint32_t nb = w.split ? 64u * K : c4;
 #pragma unroll
     for (int r = 0; r < K; ++r)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
-            if (e < c8) arena[base + e] = (uint16_t)key_to_rec16((v[0][r] >> (16 * h)) & 0xffffu);
+            const bool tum = e < nb;
+            if (e < (tum ? c4 : nb + (c8 - c4)))
+                arena[base + (tum ? e : e - nb + c4)] = (uint16_t)key_to_rec16((v[0][r] >> (16 * h)) & 0xffffu);
         }
     const uint32_t rms_t = wave_sum(a_t), rms_n = wave_sum(a_n);
     if (lane == 0) {
@@ -1422,22 +1479,23 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
     SlotRes *res = L.res[wv];
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
-    const uint32_t count = *a.deep_count < a.deep_cap ? *a.deep_count : a.deep_cap;
-    const uint32_t ngroups = (count + GB - 1) / GB;
     const Sub none = {0, 0, 0, 0, 0, 0};
-    for (uint32_t g = blockIdx.x * (SS_WIDE_BLOCK / 64) + wv; g < ngroups;
-         g += gridDim.x * (SS_WIDE_BLOCK / 64)) {
-        const uint32_t first = g * GB, nlist = count - first < GB ? count - first : GB;
+    /* the main kernel's per-wave segments, GB entries at a time */
+    for (uint32_t sg = blockIdx.x * WIDE_WAVES + wv; sg < a.deep_nseg; sg += gridDim.x * WIDE_WAVES)
+    for (uint32_t first = 0, scount = min(a.deep_seg_n[sg], a.deep_seg_cap); first < scount; first += GB) {
+        const uint32_t *list = a.deep_list + (size_t)sg * a.deep_seg_cap;
+        const uint32_t nlist = scount - first < GB ? scount - first : GB;
         /* site i's reads are in flight while site i-1 is sorted */
         uint32_t i = 0, s_cur = 0;
-        WideSite w_cur = {0, 0, 0, 0};
+        WideSite w_cur = {0, 0, 0, 0, false};
         uint32_t rd[32];
         auto describe = [&](uint32_t k, uint32_t &s, WideSite &w) {
-            s = a.deep_list[first + k];
+            s = list[first + k];
             w.ot = a.off_t[s];
             w.nt = a.off_t[s + 1] - w.ot;
             w.on = a.off_n[s];
             w.nn = a.off_n[s + 1] - w.on;
+            wide_place(w);
         };
         if (nlist) {
             describe(0, s_cur, w_cur);
