@@ -888,7 +888,12 @@ __device__ __forceinline__ bool split_fits(uint32_t nt, uint32_t nn)
     return nt <= 64u * K && nn <= 64u * K;
 }
 
-/* number of u16 keys (both halves of all K registers) below x, wave-wide */
+/* number of u16 keys (both halves of all K registers) below x, wave-wide.
+ * The empty asm pins the count where it is computed: otherwise the scheduler
+ * clusters all the compares and keeps every 64-bit ballot live (SGPR spills). */
+#ifndef SS_PIN_COUNTS
+#define SS_PIN_COUNTS 1
+#endif
 template <int K>
 __device__ __forceinline__ uint32_t count_below(const uint32_t (&v)[K], uint32_t x)
 {
@@ -898,6 +903,9 @@ __device__ __forceinline__ uint32_t count_below(const uint32_t (&v)[K], uint32_t
         c += (uint32_t)__popcll(__ballot((v[r] & 0xffffu) < x));
         c += (uint32_t)__popcll(__ballot((v[r] >> 16) < x));
     }
+#if SS_PIN_COUNTS
+    asm volatile("" : "+s"(c));
+#endif
     return c;
 }
 
