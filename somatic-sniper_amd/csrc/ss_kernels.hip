@@ -30,6 +30,29 @@
 #define SENT 0xffffffffu
 #define GMAX 8              /* sites per group (deep kernel finish)  */
 
+/* kernel tuning switches (A/B builds: make variant DEFS=-D...) */
+#ifndef SS_XOR_BANK
+#define SS_XOR_BANK 1
+#endif
+#ifndef SS_SPLIT_SORT
+#define SS_SPLIT_SORT 1   /* skip the top merge level when each sample fits in half */
+#endif
+#ifndef SS_SPLIT_WIDE
+#define SS_SPLIT_WIDE SS_SPLIT_SORT
+#endif
+#ifndef SS_OPSEL
+#define SS_OPSEL 1        /* halfswaps folded into v_pk_min/max operand selects */
+#endif
+#ifndef SS_SWZ
+#define SS_SWZ 1          /* lane xor 16 / 31 through ds_swizzle instead of VALU permutes */
+#endif
+#ifndef SS_CX_EXEC
+#define SS_CX_EXEC 0      /* exec-masked max measured slower (SALU exec writes) */
+#endif
+#ifndef SS_PIN_COUNTS
+#define SS_PIN_COUNTS 1
+#endif
+
 namespace {
 
 /* --------------------------------------------------------------------------
@@ -629,20 +652,42 @@ __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b)
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
 }
 
+/* min / max of x with halfswap(o): the swap is an operand select (op_sel),
+ * not an instruction */
+__device__ __forceinline__ uint32_t pk_min_swo(uint32_t x, uint32_t o)
+{
+#if SS_OPSEL
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(x), "v"(o));
+    return r;
+#else
+    return pk_min(x, (o >> 16) | (o << 16));
+#endif
+}
+__device__ __forceinline__ uint32_t pk_max_swo(uint32_t x, uint32_t o)
+{
+#if SS_OPSEL
+    uint32_t r;
+    asm("v_pk_max_u16 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(x), "v"(o));
+    return r;
+#else
+    return pk_max(x, (o >> 16) | (o << 16));
+#endif
+}
+/* halfswap(max(x, halfswap(o))) = max(halfswap(x), o) */
+__device__ __forceinline__ uint32_t pk_max_swx(uint32_t x, uint32_t o)
+{
+#if SS_OPSEL
+    uint32_t r;
+    asm("v_pk_max_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(x), "v"(o));
+    return r;
+#else
+    return pk_max((x >> 16) | (x << 16), o);
+#endif
+}
+
 /* x from lane ^ LJ without an LDS round trip: DPP quad permutes for 1 and 2,
  * DPP row shifts for 4 and 8, v_permlane16/32_swap for 16 and 32. */
-#ifndef SS_XOR_BANK
-#define SS_XOR_BANK 1
-#endif
-#ifndef SS_SPLIT_SORT
-#define SS_SPLIT_SORT 1   /* skip the top merge level when each sample fits in half */
-#endif
-#ifndef SS_SPLIT_WIDE
-#define SS_SPLIT_WIDE SS_SPLIT_SORT
-#endif
-#ifndef SS_CX_EXEC
-#define SS_CX_EXEC 0      /* exec-masked max measured slower (SALU exec writes) */
-#endif
 
 template <int LJ>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
@@ -654,11 +699,12 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x4e, 0xf, 0xf, false);  /* quad_perm 2,3,0,1 */
 #if SS_XOR_BANK
     } else if constexpr (LJ == 4) {
-        /* banks 0,2 read lane + 4, banks 1,3 lane - 4: two bank-masked moves */
-        const int up = __builtin_amdgcn_update_dpp(0, xi, 0x104, 0xf, 0x5, false);  /* row_shl:4 */
+        /* banks 0,2 read lane + 4, banks 1,3 lane - 4: two bank-masked moves
+         * (the first one's other banks are don't-care: no zeroed old value) */
+        const int up = __builtin_amdgcn_mov_dpp(xi, 0x104, 0xf, 0x5, false);          /* row_shl:4 */
         return (uint32_t)__builtin_amdgcn_update_dpp(up, xi, 0x114, 0xf, 0xa, false); /* row_shr:4 */
     } else if constexpr (LJ == 8) {
-        const int up = __builtin_amdgcn_update_dpp(0, xi, 0x108, 0xf, 0x3, false);  /* row_shl:8 */
+        const int up = __builtin_amdgcn_mov_dpp(xi, 0x108, 0xf, 0x3, false);          /* row_shl:8 */
         return (uint32_t)__builtin_amdgcn_update_dpp(up, xi, 0x118, 0xf, 0xc, false); /* row_shr:8 */
 #else
     } else if constexpr (LJ == 4) {
@@ -670,9 +716,19 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
         const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x118, 0xf, 0xf, false); /* row_shr:8 */
         return (lane_id() & 8u) ? dn : up;
 #endif
+#if SS_SWZ
+    } else if constexpr (LJ == 16) {
+        /* ds_swizzle bit-mask mode (and 0x1f, xor 0x10): LDS crossbar, no VALU */
+        return (uint32_t)__builtin_amdgcn_ds_swizzle(xi, 0x401f);
+    } else if constexpr (LJ == 31) {
+        return (uint32_t)__builtin_amdgcn_ds_swizzle(xi, 0x7c1f);                  /* xor 0x1f */
+#else
     } else if constexpr (LJ == 16) {
         const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
         return (lane_id() & 16u) ? r[0] : r[1];
+    } else if constexpr (LJ == 31) {
+        return xor_lane<16>(xor_lane<15>(x));
+#endif
     } else if constexpr (LJ == 32) {
         const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
         return (lane_id() & 32u) ? r[0] : r[1];
@@ -682,8 +738,6 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x141, 0xf, 0xf, false);  /* row_half_mirror */
     } else if constexpr (LJ == 15) {
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x140, 0xf, 0xf, false);  /* row_mirror */
-    } else if constexpr (LJ == 31) {
-        return xor_lane<16>(xor_lane<15>(x));
     } else {
         static_assert(LJ == 63, "unsupported lane xor");
         return xor_lane<32>(xor_lane<31>(x));
@@ -826,10 +880,10 @@ __device__ __forceinline__ void flip_stage(uint32_t (&v)[M][K])
             for (int r = 0; r < K; ++r) {
                 const int r2 = ((2 * r) ^ (int)(k - 1)) >> 1;
                 if (r2 > r) {
-                    const uint32_t sw = halfswap(v[m][r2]);
-                    const uint32_t mn = pk_min(v[m][r], sw), mx = pk_max(v[m][r], sw);
+                    const uint32_t mn = pk_min_swo(v[m][r], v[m][r2]);
+                    const uint32_t mx = pk_max_swx(v[m][r], v[m][r2]);
                     v[m][r] = mn;
-                    v[m][r2] = halfswap(mx);
+                    v[m][r2] = mx;
                 }
             }
     } else {
@@ -840,8 +894,9 @@ __device__ __forceinline__ void flip_stage(uint32_t (&v)[M][K])
             uint32_t nv[K];
 #pragma unroll
             for (int r = 0; r < K; ++r) {
-                const uint32_t o = halfswap(xor_lane<(int)mx_lane>(v[m][K - 1 - r]));
-                nv[r] = cx_lanes<lbit>(v[m][r], o);
+                const uint32_t o = xor_lane<(int)mx_lane>(v[m][K - 1 - r]);    /* halves swapped in the op */
+                const uint32_t hi = pk_max_swo(v[m][r], o), lo = pk_min_swo(v[m][r], o);
+                nv[r] = (lane_id() & (uint32_t)lbit) ? hi : lo;
             }
 #pragma unroll
             for (int r = 0; r < K; ++r) v[m][r] = nv[r];
@@ -891,9 +946,6 @@ __device__ __forceinline__ bool split_fits(uint32_t nt, uint32_t nn)
 /* number of u16 keys (both halves of all K registers) below x, wave-wide.
  * The empty asm pins the count where it is computed: otherwise the scheduler
  * clusters all the compares and keeps every 64-bit ballot live (SGPR spills). */
-#ifndef SS_PIN_COUNTS
-#define SS_PIN_COUNTS 1
-#endif
 template <int K>
 __device__ __forceinline__ uint32_t count_below(const uint32_t (&v)[K], uint32_t x)
 {
