@@ -85,6 +85,17 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+/* sums over lanes 0..31 and 32..63 (returned in lanes 31 and 63) */
+__device__ __forceinline__ uint32_t wave_halfsums(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); /* row_shr:1 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); /* row_shr:2 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); /* row_shr:4 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); /* row_shr:8 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); /* row_bcast:15 */
+    return v;
+}
+
 /* --------------------------------------------------------------------------
  * Order key of one packed read (sniper_maqcns.c:144-156 restated).
  *
@@ -693,7 +704,13 @@ template <int LJ>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
 {
     const int xi = (int)x;
-    if constexpr (LJ == 1) {
+    /* SS_SWZ >= 2 / 3: more of the lane xors through the LDS crossbar
+     * (bit-mask mode, and 0x1f, xor LJ) -- trades VALU issue for LDS latency */
+    constexpr bool swz = (SS_SWZ >= 3 && (LJ == 1 || LJ == 2 || LJ == 3 || LJ == 7 || LJ == 15)) ||
+                         (SS_SWZ >= 2 && (LJ == 4 || LJ == 8));
+    if constexpr (swz) {
+        return (uint32_t)__builtin_amdgcn_ds_swizzle(xi, 0x1f | (LJ << 10));
+    } else if constexpr (LJ == 1) {
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0xb1, 0xf, 0xf, false);  /* quad_perm 1,0,3,2 */
     } else if constexpr (LJ == 2) {
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x4e, 0xf, 0xf, false);  /* quad_perm 2,3,0,1 */
@@ -1007,8 +1024,8 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             k1 = in1 ? k1 : 0xffffu;
             const uint32_t t0 = min(rd0 & 0x7fu, cap), t1 = min(rd1 & 0x7fu, cap);
             const uint32_t x = (in0 ? t0 * t0 : 0u) + (in1 ? t1 * t1 : 0u);
-            a_t += tum ? x : 0u;
-            a_n += tum ? 0u : x;
+            a_t += tum ? x : 0u;                      /* tumor part (non-split) */
+            a_n += x;                                 /* both samples */
             v[m][r] = k0 | k1 << 16;
         }
         rs_t[m] = a_t;
@@ -1044,8 +1061,19 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
                 }
             }
         }
-        const uint32_t rms_t = (diag & 128u) ? rs_t[m] : wave_sum(rs_t[m]);
-        const uint32_t rms_n = (diag & 128u) ? rs_n[m] : wave_sum(rs_n[m]);
+        /* rms sums: split placement has one sample per half-wave */
+        uint32_t rms_t, rms_n;
+        if (diag & 128u) {
+            rms_t = rs_t[m];
+            rms_n = rs_n[m];
+        } else if (split) {
+            const uint32_t h = wave_halfsums(rs_n[m]);
+            rms_t = (uint32_t)__builtin_amdgcn_readlane((int)h, 31);
+            rms_n = (uint32_t)__builtin_amdgcn_readlane((int)h, 63);
+        } else {
+            rms_t = wave_sum(rs_t[m]);
+            rms_n = wave_sum(rs_n[m]) - rms_t;
+        }
         if (lane == 0) {
             Slot3 &st_t = slot[2 * m], &st_n = slot[2 * m + 1];
             st_t.rec_n = bt | nt << 16;
