@@ -625,9 +625,9 @@ __device__ __forceinline__ void nt_tables(uint32_t ref16, uint32_t &tb, uint32_t
  *   bits 24..31 strand << 4 (the field offset of its w counter, see fold_sample) */
 __device__ __forceinline__ uint32_t key_to_rec(uint32_t k)
 {
-    const uint32_t minq = (k >> 5) & 0xffu, st = (k >> 3) & 1u, nz = k & 1u;
-    const uint32_t q = (minq < 4u && nz) ? 4u : minq;
-    return q | 1u << 16 | st << 28;
+    /* q = (minq < 4 && nz) ? 4 : minq  ==  max(minq, nz * 4) */
+    const uint32_t q = max((k >> 5) & 0xffu, (k & 1u) << 2);
+    return q | 1u << 16 | (k & 8u) << 25;
 }
 
 /* 16-bit fold record (wide kernel, whose LDS arena holds 16 deep sites):
@@ -635,9 +635,8 @@ __device__ __forceinline__ uint32_t key_to_rec(uint32_t k)
  * (r >> 8) & 31 is strand << 4 like the u32 record's top byte. */
 __device__ __forceinline__ uint32_t key_to_rec16(uint32_t k)
 {
-    const uint32_t minq = (k >> 5) & 0xffu, st = (k >> 3) & 1u, nz = k & 1u;
-    const uint32_t q = (minq < 4u && nz) ? 4u : minq;
-    return q | st << 12 | 1u << 13;
+    const uint32_t q = max((k >> 5) & 0xffu, (k & 1u) << 2);
+    return q | (k & 8u) << 9 | 1u << 13;
 }
 
 template <typename RecT> struct RecForm;
@@ -1047,17 +1046,30 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             c7 = count_below<K>(v[m], 7u << 13); c8 = count_below<K>(v[m], 0xffffu);
         }
         /* fold records back over the staged reads: tumor run, normal run */
+        if (split) {
+            /* one sample per half-wave: a per-lane base, constant offsets */
+            const bool tl = lane < 32u;
+            const uint32_t e0 = lane * (2u * K);
+            const uint32_t lim = tl ? c4 : 64u * K + (c8 - c4);
+            uint32_t *rl0 = rec + ((tl ? bt : bn - 64u * K) + e0);
 #pragma unroll
-        for (int r = 0; r < K; ++r) {
+            for (int r = 0; r < K; ++r)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
-                const uint32_t key = (v[m][r] >> (16 * h)) & 0xffffu;
-                const uint32_t nb = split ? 64u * K : c4;     /* first element of the normal run */
-                const bool tum = e < nb;
-                if (e < (tum ? c4 : nb + (c8 - c4)) && !(diag & 64u)) {
-                    const uint32_t idx = tum ? bt + e : bn + (e - nb);
-                    rec[idx] = key_to_rec(key);
+                for (int h = 0; h < 2; ++h)
+                    if (e0 + 2u * r + (uint32_t)h < lim && !(diag & 64u))
+                        rl0[2 * r + h] = key_to_rec((v[m][r] >> (16 * h)) & 0xffffu);
+        } else {
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
+                    const uint32_t key = (v[m][r] >> (16 * h)) & 0xffffu;
+                    const bool tum = e < c4;
+                    if (e < c8 && !(diag & 64u)) {
+                        const uint32_t idx = tum ? bt + e : bn + (e - c4);
+                        rec[idx] = key_to_rec(key);
+                    }
                 }
             }
         }
