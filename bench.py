@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0x5EED5A1DC0FFEE01)
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", default="nccl",
+                    help="process-group backend for N>1 (nccl = RCCL; gloo rehearses N ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -91,10 +93,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend != "nccl":
+        local %= max(1, torch.cuda.device_count())   # rehearsal: ranks share the visible GPUs
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -200,8 +207,6 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
     if world > 1:
         dist.destroy_process_group()
 

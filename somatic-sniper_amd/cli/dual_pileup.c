@@ -1,6 +1,8 @@
 /* dual_pileup.c -- see dual_pileup.h for the behaviour being reproduced. */
 #include "dual_pileup.h"
 
+#include "column_pileup.h"
+
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -314,9 +316,44 @@ static int stream_next(stream_t *S, int32_t *tid, int32_t *pos, const uint32_t *
     return h[2];
 }
 
+/* Column mode: both samples' reported columns (column_pileup.h), merged in
+ * (tid, pos) order.  The lockstep loop of the walk reports exactly the
+ * positions both walks report with entries: a walk that moves to a later
+ * contig has no entries left on the earlier one, so the positions it skips
+ * the other walk through are never shared. */
+static int column_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, dual_site_fn fn,
+                      void *data)
+{
+    col_stream_t *a = col_stream_start(fp1, mask, thresh), *b = col_stream_start(fp2, mask, thresh);
+    if (!a || !b) { fprintf(stderr, "out of memory\n"); exit(1); }
+    int32_t t1, p1, t2, p2;
+    int r1, r2, np1, np2;
+    const uint32_t *pk1, *pk2;
+    int v1 = col_stream_next(a, &t1, &p1, &r1, &pk1, &np1);
+    int v2 = col_stream_next(b, &t2, &p2, &r2, &pk2, &np2);
+    while (v1 && v2) {
+        if (t1 < t2 || (t1 == t2 && p1 < p2)) {
+            v1 = col_stream_next(a, &t1, &p1, &r1, &pk1, &np1);
+        } else if (t2 < t1 || p2 < p1) {
+            v2 = col_stream_next(b, &t2, &p2, &r2, &pk2, &np2);
+        } else {
+            if (fn(t1, p1, r1, r2, pk1, np1, pk2, np2, data)) break;
+            v1 = col_stream_next(a, &t1, &p1, &r1, &pk1, &np1);
+            v2 = col_stream_next(b, &t2, &p2, &r2, &pk2, &np2);
+        }
+    }
+    const int e1 = col_stream_stop(a), e2 = col_stream_stop(b);
+    if (e1 || e2) {
+        fprintf(stderr, "[dual_pileup] truncated or malformed BAM record\n");
+        return -1;
+    }
+    return 0;
+}
+
 int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, int threaded,
                     dual_site_fn fn, void *data)
 {
+    if (threaded == 2) return column_run(fp1, fp2, mask, thresh, fn, data);
     walker_t *w1 = (walker_t *)malloc(sizeof(walker_t)), *w2 = (walker_t *)malloc(sizeof(walker_t));
     if (!w1 || !w2) { free(w1); free(w2); return -1; }
     walker_init(w1, fp1, mask, thresh);

@@ -31,10 +31,14 @@ typedef int (*dual_site_fn)(int32_t tid, int32_t pos, int n1, int n2, const uint
                             const uint32_t *pk2, int np2, void *data);
 
 /* mask < 0 selects SS_BAM_DEF_MASK, otherwise SS_BAM_FUNMAP | mask
- * (bam_plbuf_set_mask :148-152); thresh < 0 is 0.  threaded != 0 runs each
- * sample's walk on its own thread (the two walks only meet in the lockstep
- * loop, so the reported sites are the same).  Returns 0, or -1 on a read
- * error (message on stderr). */
+ * (bam_plbuf_set_mask :148-152); thresh < 0 is 0.  threaded: 0 walks both
+ * samples position by position on the calling thread; 1 runs each sample's
+ * walk on its own thread (the two walks only meet in the lockstep loop, so
+ * the reported sites are the same); 2 builds each sample's columns by
+ * scattering reads over windows of positions on its own thread
+ * (column_pileup.h) and merges the two column streams -- same sites, same
+ * entries in the same order, a fraction of the work per entry.  Returns 0,
+ * or -1 on a read error (message on stderr). */
 int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, int threaded,
                     dual_site_fn fn, void *data);
 

@@ -19,7 +19,8 @@
  *
  * Environment: SS_DEVICE (GPU index, default 0), SS_BATCH (sites per batch,
  * default 2^20), SS_BGZF_THREADS (inflate threads per BAM, default 4),
- * SS_PILEUP_THREADS (1: tumor and normal walks on their own threads, 0: one thread),
+ * SS_PILEUP_THREADS (2, default: column pileup, one thread per sample;
+ * 1: tumor and normal walks on their own threads; 0: one thread),
  * SS_DUMP_PILEUP=FILE (test hook: also write every reported site, see
  * dump_site()), SS_PILEUP_ONLY=1 (test / timing hook: walk (and dump) without
  * scoring, so the pileup restatement is testable on a host without a GPU; no
@@ -369,7 +370,7 @@ int main(int argc, char *argv[])
     pthread_cond_init(&R.cv, NULL);
     R.pileup_only = pileup_only;
     pthread_create(&R.th, NULL, scorer_main, &R);
-    dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, env_int("SS_PILEUP_THREADS", 1), on_site, &R);
+    dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, env_int("SS_PILEUP_THREADS", 2), on_site, &R);
     if (R.bat[R.fill].n) submit(&R);
     pthread_mutex_lock(&R.mu);
     R.quit = 1;

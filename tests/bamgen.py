@@ -16,7 +16,7 @@ import zlib
 import numpy as np
 
 SEQ_CODES = "=ACMGRSVTWYHKDBN"
-CIGAR_OPS = "MIDNSHP"
+CIGAR_OPS = "MIDNSHP=X"
 
 
 def reg2bin(beg, end):
@@ -65,7 +65,7 @@ def encode_record(tid, pos, name, mapq, flag, cigar, seq, qual):
     return struct.pack("<i", len(body)) + body
 
 
-def write_bam(path, contigs, records):
+def write_bam(path, contigs, records, disorder=None):
     text = "@HD\tVN:1.0\tSO:coordinate\n" + "".join(
         f"@SQ\tSN:{n}\tLN:{len(s)}\n" for n, s in contigs)
     hdr = b"BAM\1" + struct.pack("<i", len(text)) + text.encode() + struct.pack("<i", len(contigs))
@@ -73,6 +73,13 @@ def write_bam(path, contigs, records):
         nb = n.encode() + b"\0"
         hdr += struct.pack("<i", len(nb)) + nb + struct.pack("<i", len(s))
     recs = sorted(records, key=lambda r: (r[0] if r[0] >= 0 else 1 << 30, r[1]))   # unmapped (tid -1) last
+    if disorder is not None:
+        # positions out of order within a contig (the reference checks only the
+        # contig order): some records move a few places back in the file
+        for i in disorder.choice(len(recs), max(1, len(recs) // 40), replace=False):
+            j = max(0, int(i) - int(disorder.integers(1, 12)))
+            if recs[j][0] == recs[i][0]:
+                recs.insert(j, recs.pop(int(i)))
     data = hdr + b"".join(encode_record(*r) for r in recs)
     with open(path, "wb") as f:
         f.write(bgzf_blocks(data))
@@ -87,14 +94,18 @@ def write_fasta(path, contigs, width=60):
 
 
 def make_pair(outdir, seed=1, lengths=(3000, 2200, 1500, 800), depth_t=30, depth_n=24,
-              read_len=(40, 100), exotic=True, names=None, empty_normal=False, unmapped=False):
+              read_len=(40, 100), exotic=True, names=None, empty_normal=False, unmapped=False,
+              odd_cigars=False, unsorted=False):
     """Returns paths (fasta, tumor_bam, normal_bam).
 
     names: contig names (default chr1..); the reference looks them up in the
     FASTA index with fai_fetch's region parser, so ':' and ',' in a name
     matter.  empty_normal: a normal BAM with a header and no reads.
     unmapped: add flag-0x4 reads, placed next to a mate and at the tail
-    (tid -1), to both samples."""
+    (tid -1), to both samples.  odd_cigars: also reads with no reference
+    span (all soft clip / insertion), leading deletions, H and P ops, '=' / 'X'
+    ops (samtools 0.1.6 moves neither coordinate for them) and long reference
+    skips.  unsorted: positions out of order within a contig."""
     rng = np.random.default_rng(seed)
     contigs = []
     for ci, L in enumerate(lengths):
@@ -144,6 +155,13 @@ def make_pair(outdir, seed=1, lengths=(3000, 2200, 1500, 800), depth_t=30, depth
                 elif exotic and r < 0.15:
                     a = int(rng.integers(5, rl - 5)); gap = int(rng.integers(5, 40))
                     cigar = [("M", a), ("N", gap), ("M", rl - a)]
+                elif odd_cigars and r < 0.25:
+                    a = int(rng.integers(5, rl - 10)); b = int(rng.integers(1, 5))
+                    cigar = [[("S", rl)], [("I", 3), ("S", rl - 3)], [("D", 3), ("M", rl)],
+                             [("H", 5), ("M", a), ("P", 2), ("I", b), ("M", rl - a - b), ("H", 4)],
+                             [("M", a), ("=", b), ("M", rl - a - b)], [("M", a), ("X", b), ("D", 2), ("M", rl - a - b)],
+                             [("S", 4), ("M", a), ("N", 300), ("M", rl - a - 4)],
+                             [("M", a), ("D", 2), ("N", 7), ("I", b), ("M", rl - a - b)]][int(rng.integers(0, 8))]
                 else:
                     cigar = [("M", rl)]
                 # read bases following the cigar
@@ -169,9 +187,9 @@ def make_pair(outdir, seed=1, lengths=(3000, 2200, 1500, 800), depth_t=30, depth
                                 b = str(rng.choice(list("MRWSYKVHDB")))
                             seq.append(b)
                             rp += 1
-                    elif op in "IS":
+                    elif op in "IS=X":
                         seq += list(rng.choice(list("ACGT"), n))
-                    else:
+                    elif op in "DN":
                         rp += n
                 q = rng.integers(2, 42, len(seq))
                 if exotic:
@@ -204,8 +222,8 @@ def make_pair(outdir, seed=1, lengths=(3000, 2200, 1500, 800), depth_t=30, depth
     tb = os.path.join(outdir, "tumor.bam")
     nb = os.path.join(outdir, "normal.bam")
     write_fasta(fa, contigs)
-    write_bam(tb, contigs, reads_for("t", depth_t))
-    write_bam(nb, contigs, [] if empty_normal else reads_for("n", depth_n))
+    write_bam(tb, contigs, reads_for("t", depth_t), rng if unsorted else None)
+    write_bam(nb, contigs, [] if empty_normal else reads_for("n", depth_n), rng if unsorted else None)
     return fa, tb, nb
 
 

@@ -48,7 +48,8 @@ def datasets(tmp_path_factory):
     for seed, kw in [(1, {}), (2, dict(depth_t=60, depth_n=30)), (3, dict(exotic=False, lengths=(5000,))),
                      (4, dict(lengths=(400, 300, 900, 200, 700), depth_t=15, depth_n=12)),
                      (5, dict(lengths=(600, 500, 400, 500, 300), names=NAMES, unmapped=True)),
-                     (6, dict(lengths=(700, 300), empty_normal=True))]:
+                     (6, dict(lengths=(700, 300), empty_normal=True)),
+                     (7, dict(lengths=(900, 600, 500, 700), odd_cigars=True, unsorted=True))]:
         d = tmp_path_factory.mktemp(f"pair{seed}")
         bamgen.make_pair(str(d), seed=seed, **kw)
         out.append((str(d), "ref.fa", "tumor.bam", "normal.bam"))
@@ -70,9 +71,10 @@ def _dump(cli, d, fa, t, n, opts, native, threads="1"):
 @need_native
 @need_dump
 @pytest.mark.parametrize("opts", [[], ["-q", "20"], ["-q", "61"]])
-@pytest.mark.parametrize("threads", ["1", "0"])
+@pytest.mark.parametrize("threads", ["2", "1", "0"])
 def test_pileup_site_stream_matches_reference(datasets, opts, threads):
-    """threads: the tumor and normal walks on their own threads, or both on one."""
+    """threads: column pileup (2), the tumor and normal walks on their own threads (1), or
+    both walks on one thread (0)."""
     for d, fa, t, n in datasets:
         ref = _dump(REF_DUMP, d, fa, t, n, opts, native=False)
         nat = _dump(NATIVE, d, fa, t, n, opts, native=True, threads=threads)
