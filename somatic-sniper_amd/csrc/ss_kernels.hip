@@ -52,6 +52,31 @@
 #ifndef SS_PIN_COUNTS
 #define SS_PIN_COUNTS 1
 #endif
+#ifndef SS_STAMP
+#define SS_STAMP 0        /* diagnostic builds: per-phase s_memtime cycle totals of the main kernel */
+#endif
+
+/* Phase stamps (SS_STAMP builds only): wave-uniform cycle accumulators,
+ * summed over waves into ss_stamp_acc at exit; read by ss_debug_stamps(). */
+#define SS_NSTAMP 16
+#if SS_STAMP
+__device__ unsigned long long ss_stamp_acc[SS_NSTAMP];
+struct Stamps {
+    uint64_t prev, acc[SS_NSTAMP];
+    __device__ void start() { prev = __builtin_amdgcn_s_memtime(); for (int i = 0; i < SS_NSTAMP; ++i) acc[i] = 0; }
+    __device__ void mark(int i) { const uint64_t t = __builtin_amdgcn_s_memtime(); acc[i] += t - prev; prev = t; }
+    __device__ void flush() {
+        if (__lane_id() == 0)
+            for (int i = 0; i < SS_NSTAMP; ++i) atomicAdd(&ss_stamp_acc[i], (unsigned long long)acc[i]);
+    }
+};
+#else
+struct Stamps {
+    __device__ void start() {}
+    __device__ void mark(int) {}
+    __device__ void flush() {}
+};
+#endif
 
 namespace {
 
@@ -986,7 +1011,7 @@ struct SiteA {
 
 template <int K, int M>
 __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M], uint32_t cap,
-                                           Slot3 *slot, uint32_t diag)
+                                           Slot3 *slot, uint32_t diag, Stamps &st)
 {
     const uint32_t lane = lane_id();
     uint32_t v[M][K];
@@ -1030,7 +1055,9 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
         rs_t[m] = a_t;
         rs_n[m] = a_n;
     }
+    st.mark(7);
     if (!(diag & 1u)) packed_bitonic_flip<M, K>(v, !split);
+    st.mark(8);
     uint32_t *rec = stage;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -1045,6 +1072,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             c5 = count_below<K>(v[m], 5u << 13); c6 = count_below<K>(v[m], 6u << 13);
             c7 = count_below<K>(v[m], 7u << 13); c8 = count_below<K>(v[m], 0xffffu);
         }
+        st.mark(9);
         /* fold records back over the staged reads: tumor run, normal run */
         if (split) {
             /* one sample per half-wave: a per-lane base, constant offsets */
@@ -1097,6 +1125,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             st_n.cnt23 = (c7 - c6) | (c8 - c7) << 16;
             st_n.rms = rms_n;
         }
+        st.mark(10);
     }
 }
 
@@ -1175,9 +1204,38 @@ __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s
 #define D_REF(i) rl(desc, 17u + (i))
 #define D_N(i) rl(desc, 33u + (i))
 
-/* Hand every site of the block (descriptor `desc`) that needs more sort
- * slots than the packed main-kernel sort (PK_MAX, incl. the pad element) to
- * the wide kernel: one atomic per block, not per site. */
+/* Site sizes of a block (descriptor `desc`), lane i = site i: the inclusive
+ * prefix sum of the sites' read counts (DPP row scan over lanes 0..15) and
+ * the mask of sites that need more sort slots than the packed main-kernel
+ * sort (PK_MAX, incl. the pad element).  Recomputed where needed rather than
+ * kept live across the block (register pressure). */
+struct BlockScan {
+    uint32_t incl;        /* per lane: reads of sites 0..lane */
+    uint64_t deep;        /* wave-uniform */
+};
+
+__device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
+{
+    const uint32_t lane = lane_id();
+    /* lane i (< 16): off_t[i] is desc itself, off_t[i + 1] the next lane's
+     * (DPP wave_shl:1); off_n[i] comes from lane 33 + i */
+    const uint32_t n0 = (uint32_t)__shfl((int)desc, 33 + (int)lane);
+    const uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)desc, 0x130, 0xf, 0xf, false) - desc;
+    const uint32_t nn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n0, 0x130, 0xf, 0xf, false) - n0;
+    const uint32_t sz = lane < nsite ? nt + nn : 0u;
+    BlockScan r;
+    r.deep = __ballot(lane < nsite && sz + (nt & 1u) > PK_MAX);
+    int x = (int)sz;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);    /* row_shr:1 */
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);    /* row_shr:2 */
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);    /* row_shr:4 */
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);    /* row_shr:8 */
+    r.incl = (uint32_t)x;
+    return r;
+}
+
+/* Hand every site of the block that is too deep for the packed sort to the
+ * wide kernel: one list push per block, not per site. */
 __device__ __forceinline__ void push_block_deep(const ss_score_args &a, uint32_t desc, uint32_t nsite,
                                                 uint64_t sblk, uint32_t *seg, uint32_t &ndeep)
 {
@@ -1203,44 +1261,57 @@ struct Sub {
     uint32_t n0, ln;      /* normal read run */
 };
 
-/* Largest run of sites from `pos` whose reads fit one staging buffer; a site
- * too deep for the packed sort is left to the deep kernel. */
-__device__ __forceinline__ Sub form_sub(const ss_score_args &a, uint32_t desc, uint32_t nsite,
-                                        uint32_t pos, uint64_t sblk)
+/* staged u32 available to one sub-group: the tumor run is rounded up to a
+ * multiple of 4 (16-byte LDS-DMA pieces) before the normal run */
+#define STG_RUNS (STG - 3)
+
+/* Largest run of sites from `pos` whose reads fit one staging buffer; sites
+ * too deep for the packed sort (listed by scan_block) are skipped at the
+ * start of a run and end it elsewhere.  Wave-parallel over the block. */
+__device__ __forceinline__ Sub form_sub(uint32_t desc, uint32_t nsite, uint32_t pos)
 {
-    uint32_t i = pos, tot = 0;
-    while (i < nsite) {
-        const uint32_t ntl = D_T(i + 1u) - D_T(i);
-        const uint32_t sz = ntl + (D_N(i + 1u) - D_N(i));
-        if (sz + (ntl & 1u) > PK_MAX) {        /* sort slots incl. the pad element */
-            if (i == pos) { pos = ++i; continue; }     /* listed by push_block_deep */
-            break;
-        }
-        if (tot + sz > STG) break;
-        tot += sz;
-        ++i;
-    }
+    const uint32_t lane = lane_id();
+    const BlockScan bs = scan_block(desc, nsite);
+    const uint64_t valid = (1ull << nsite) - 1ull;                 /* nsite <= GB < 64 */
+    const uint64_t nd = ~bs.deep & valid & ~((1ull << pos) - 1ull);
     Sub r;
+    if (nd == 0) {
+        pos = nsite;
+        r.b = nsite;
+    } else {
+        pos = (uint32_t)__builtin_ctzll(nd);
+        const uint32_t base = pos ? rl(bs.incl, pos - 1u) : 0u;
+        const bool stop = lane > pos && lane < nsite && (((bs.deep >> lane) & 1ull) || bs.incl - base > STG_RUNS);
+        const uint64_t m = __ballot(stop);
+        r.b = m ? (uint32_t)__builtin_ctzll(m) : nsite;
+    }
     r.a = pos;
-    r.b = i;
     r.t0 = D_T(pos);
-    r.lt = D_T(i) - r.t0;
+    r.lt = D_T(r.b) - r.t0;
     r.n0 = D_N(pos);
-    r.ln = D_N(i) - r.n0;
+    r.ln = D_N(r.b) - r.n0;
     return r;
+}
+
+/* offset of the normal run in the stage */
+__device__ __forceinline__ uint32_t normal_base(const Sub &r) { return (r.lt + 3u) & ~3u; }
+
+/* n u32 from src into LDS dst by LDS-DMA: 16-byte pieces, then up to 3 single words */
+__device__ __forceinline__ void dma_run(const uint32_t *src, uint32_t n, uint32_t *dst)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t n4 = n & ~3u;
+    for (uint32_t i = 0; i < n4; i += 256u)
+        if (i + 4u * lane < n4)
+            __builtin_amdgcn_global_load_lds((glb_void_t *)(src + i + 4u * lane), (lds_void_t *)(dst + i), 16, 0, 0);
+    if (lane < n - n4)
+        __builtin_amdgcn_global_load_lds((glb_void_t *)(src + n4 + lane), (lds_void_t *)(dst + n4), 4, 0, 0);
 }
 
 __device__ __forceinline__ void issue_dma(const ss_score_args &a, const Sub &r, uint32_t *buf)
 {
-    const uint32_t lane = lane_id();
-    for (uint32_t i = 0; i < r.lt; i += 64u)
-        if (i + lane < r.lt)
-            __builtin_amdgcn_global_load_lds((glb_void_t *)(a.reads_t + r.t0 + i + lane),
-                                             (lds_void_t *)(buf + i), 4, 0, 0);
-    for (uint32_t i = 0; i < r.ln; i += 64u)
-        if (i + lane < r.ln)
-            __builtin_amdgcn_global_load_lds((glb_void_t *)(a.reads_n + r.n0 + i + lane),
-                                             (lds_void_t *)(buf + r.lt + i), 4, 0, 0);
+    dma_run(a.reads_t + r.t0, r.lt, buf);
+    dma_run(a.reads_n + r.n0, r.ln, buf + normal_base(r));
 }
 
 /* Phases B, C, D for the G sites of a sub-group.  Fold records are RecT
@@ -1249,7 +1320,7 @@ template <typename RecT>
 __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const RecT *recs, uint32_t *stage,
                                            const Slot3 *slot, SlotRes *res, const uint32_t *sites,
                                            const uint32_t *refcs, const double *fk,
-                                           bool have_next, const Sub &nxt, uint32_t diag)
+                                           bool have_next, const Sub &nxt, uint32_t diag, Stamps &st)
 {
     const uint32_t lane = lane_id();
     const int sl = (int)(lane >> 1);               /* slot = site * 2 + sample */
@@ -1276,10 +1347,12 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     /* every fold record has been read: the next sub-group's reads may now
      * stream into the stage while the likelihoods are computed */
     wave_sync();
+    st.mark(3);
     if (have_next) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         issue_dma(a, nxt, stage);
     }
+    st.mark(11);
     /* exchange esum / fsum within the lane pair (DPP, all lanes active) */
     float es[4], fs[4];
 #pragma unroll
@@ -1305,6 +1378,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         p[t] = role ? o : mine[t];
         p[5 + t] = role ? mine[t] : o;
     }
+    st.mark(12);
     if (act && role == 0u) {
         uint32_t lk[10], min_lk, rms_q, cns;
         if (!(diag & 4u)) glf_finish(p, es, depth, rms, a.m, lk, min_lk, rms_q, cns);
@@ -1327,12 +1401,14 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         }
     }
     wave_sync();
+    st.mark(4);
     if ((int)lane < G) {
         /* the decision reads both samples' records straight from LDS */
         if (!(diag & 8u)) decide_site(a, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
         else a.score[sites[lane]] = (int32_t)res[2 * lane].cns;
     }
     wave_sync();
+    st.mark(5);
 }
 
 }  // namespace
@@ -1350,6 +1426,8 @@ void ss_score_main(ss_score_args a)
     const uint32_t wv = threadIdx.x >> 6;
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
+    Stamps st;
+    st.start();
 
     uint32_t *stage = L.stage[wv];
     Slot3 *slot = L.slot[wv];
@@ -1366,6 +1444,7 @@ void ss_score_main(ss_score_args a)
     uint32_t ndeep = 0;
     if (blk >= nblocks) {
         if (lane == 0) a.deep_seg_n[gw] = 0u;
+        st.flush();
         return;
     }
     uint32_t desc = load_desc(a, blk * GB);
@@ -1373,11 +1452,12 @@ void ss_score_main(ss_score_args a)
     uint64_t nblk = blk + nwaves;
     uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
     push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
-    Sub cur = form_sub(a, desc, nsite, 0, blk * GB);
+    Sub cur = form_sub(desc, nsite, 0);
     while (cur.a == cur.b) {               /* whole block deep */
         blk = nblk;
         if (blk >= nblocks) {
             if (lane == 0) a.deep_seg_n[gw] = ndeep;
+            st.flush();
             return;
         }
         desc = ndesc;
@@ -1385,12 +1465,14 @@ void ss_score_main(ss_score_args a)
         nblk = blk + nwaves;
         ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
         push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
-        cur = form_sub(a, desc, nsite, 0, blk * GB);
+        cur = form_sub(desc, nsite, 0);
     }
     issue_dma(a, cur, stage);
+    st.mark(6);
 
     for (;;) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the sub-group's reads are in LDS */
+        st.mark(0);
         /* ---- phase A ---- */
         int G = 0;
         for (uint32_t i = cur.a; i < cur.b;) {
@@ -1404,7 +1486,7 @@ void ss_score_main(ss_score_args a)
                 S2[m].nt = D_T(j + 1u) - t_i;
                 S2[m].nn = D_N(j + 1u) - n_i;
                 S2[m].bt = t_i - cur.t0;
-                S2[m].bn = cur.lt + (n_i - cur.n0);
+                S2[m].bn = normal_base(cur) + (n_i - cur.n0);
                 S2[m].ref16 = rdesc >> 8;
                 tot[m] = S2[m].nt + (S2[m].nt & 1u) + S2[m].nn;   /* sort slots incl. pad */
                 if (lane == 0 && i + (uint32_t)m < cur.b) {
@@ -1413,25 +1495,26 @@ void ss_score_main(ss_score_args a)
                 }
             }
             if (i + 1u < cur.b && tot[0] <= 256u && tot[1] <= 256u) {   /* two sites, interleaved */
-                if (tot[0] <= 128u && tot[1] <= 128u) sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, diag);
-                else sort_sites<2, 2>(stage, S2, cap, slot + 2 * G, diag);
+                if (tot[0] <= 128u && tot[1] <= 128u) sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, diag, st);
+                else sort_sites<2, 2>(stage, S2, cap, slot + 2 * G, diag, st);
                 G += 2;
                 i += 2;
                 continue;
             }
             SiteA S1[1] = {S2[0]};
-            if (tot[0] <= 128u) sort_sites<1, 1>(stage, S1, cap, slot + 2 * G, diag);
-            else if (tot[0] <= 256u) sort_sites<2, 1>(stage, S1, cap, slot + 2 * G, diag);
-            else sort_sites<4, 1>(stage, S1, cap, slot + 2 * G, diag);
+            if (tot[0] <= 128u) sort_sites<1, 1>(stage, S1, cap, slot + 2 * G, diag, st);
+            else if (tot[0] <= 256u) sort_sites<2, 1>(stage, S1, cap, slot + 2 * G, diag, st);
+            else sort_sites<4, 1>(stage, S1, cap, slot + 2 * G, diag, st);
             ++G;
             ++i;
         }
         wave_sync();
+        st.mark(1);
         /* ---- next sub-group: same block, else the next non-empty block ---- */
         Sub nxt;
         bool have = false;
         if (cur.b < nsite) {
-            nxt = form_sub(a, desc, nsite, cur.b, blk * GB);
+            nxt = form_sub(desc, nsite, cur.b);
             have = nxt.a < nxt.b;
         }
         while (!have) {
@@ -1442,15 +1525,17 @@ void ss_score_main(ss_score_args a)
             nblk = blk + nwaves;
             ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
             push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
-            nxt = form_sub(a, desc, nsite, 0, blk * GB);
+            nxt = form_sub(desc, nsite, 0);
             have = nxt.a < nxt.b;
         }
+        st.mark(2);
         /* ---- phases B + C + D (the next DMA is issued after the fold) ---- */
-        finish_sub<uint32_t>(a, G, stage, stage, slot, res, sites, refcs, fk, have, nxt, diag);
+        finish_sub<uint32_t>(a, G, stage, stage, slot, res, sites, refcs, fk, have, nxt, diag, st);
         if (!have) break;
         cur = nxt;
     }
     if (lane == 0) a.deep_seg_n[gw] = ndeep;
+    st.flush();
 }
 
 /* --------------------------------------------------------------------------
@@ -1639,7 +1724,8 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 ++G;
             }
             wave_sync();
-            if (G) finish_sub<uint16_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, 0u);
+            Stamps nost;
+            if (G) finish_sub<uint16_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, 0u, nost);
         }
     }
 }
@@ -1843,3 +1929,18 @@ int ss_launch_synth_reads(const ss_synth_k_t &k, uint64_t first, uint64_t n,
                        off_t, off_n, rt, rn);
     return (int)hipGetLastError();
 }
+
+#if SS_STAMP
+/* diagnostic builds: per-phase cycle totals of ss_score_main (summed over
+ * waves), then reset.  Phases: 0 wait for the staged reads, 1 phase A loop
+ * remainder, 2 next sub-group, 3 fold, 4 glf finish + stores, 5 decision,
+ * 6 prologue, 7 key build, 8 sort network, 9 group counts, 10 record
+ * write-back + rms, 11 DMA issue, 12 genotype likelihoods. */
+extern "C" __attribute__((visibility("default"))) int ss_debug_stamps(unsigned long long *out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ss_stamp_acc), sizeof(unsigned long long) * SS_NSTAMP) != hipSuccess)
+        return -1;
+    static const unsigned long long zero[SS_NSTAMP] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(ss_stamp_acc), zero, sizeof zero) == hipSuccess ? 0 : -1;
+}
+#endif
