@@ -52,6 +52,21 @@
 #ifndef SS_PIN_COUNTS
 #define SS_PIN_COUNTS 1
 #endif
+#ifndef SS_ASM_HALVES
+#define SS_ASM_HALVES 1   /* in-register half compare-exchange as hand-written SDWA pairs */
+#endif
+#ifndef SS_FOLD_UNROLL
+#define SS_FOLD_UNROLL 2
+#endif
+/* `#pragma unroll N` with N from a macro: the count reaches the pragma expanded */
+#define SS_PRAGMA(x) _Pragma(#x)
+#define SS_UNROLL(n) SS_PRAGMA(unroll n)
+#ifndef SS_PRIO_FOLD
+#define SS_PRIO_FOLD 0    /* wave priority raised over the fold's dependency chain */
+#endif
+#ifndef SS_PRIO_SORT
+#define SS_PRIO_SORT 0    /* wave priority raised over the sort network */
+#endif
 #ifndef SS_STAMP
 #define SS_STAMP 0        /* diagnostic builds: per-phase s_memtime cycle totals of the main kernel */
 #endif
@@ -586,7 +601,10 @@ __device__ __forceinline__ void finish_group(const ss_score_args &a, int G, cons
  * then evaluates the 10 genotypes.  Phase D: lane s decides site s.
  * ------------------------------------------------------------------------ */
 #define GB 16               /* sites per block                 */
-#define STG 2048            /* staged u32 per wave             */
+#ifndef SS_STG
+#define SS_STG 2048
+#endif
+#define STG SS_STG          /* staged u32 per wave             */
 #define PK_MAX 512          /* nT + nN handled by the packed sort (K <= 4) */
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -837,6 +855,10 @@ __device__ __forceinline__ uint32_t cx_lanes(uint32_t x, uint32_t o)
  * (cx_halves2: two registers interleaved) or one wait state separates them. */
 __device__ __forceinline__ uint32_t cx_halves(uint32_t x)
 {
+#if !SS_ASM_HALVES
+    const uint32_t lo = x & 0xffffu, hi = x >> 16;
+    return min(lo, hi) | max(lo, hi) << 16;
+#endif
     uint32_t r;
     asm volatile("v_max_u16_sdwa %0, %1, %1 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
                  "s_nop 0\n\t"
@@ -848,6 +870,11 @@ __device__ __forceinline__ uint32_t cx_halves(uint32_t x)
 
 __device__ __forceinline__ void cx_halves2(uint32_t &x0, uint32_t &x1)
 {
+#if !SS_ASM_HALVES
+    x0 = cx_halves(x0);
+    x1 = cx_halves(x1);
+    return;
+#endif
     uint32_t r0, r1;
     asm volatile("v_max_u16_sdwa %0, %2, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
                  "v_max_u16_sdwa %1, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
@@ -1056,7 +1083,9 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
         rs_n[m] = a_n;
     }
     st.mark(7);
+    if (SS_PRIO_SORT) __builtin_amdgcn_s_setprio(SS_PRIO_SORT);
     if (!(diag & 1u)) packed_bitonic_flip<M, K>(v, !split);
+    if (SS_PRIO_SORT) __builtin_amdgcn_s_setprio(0);
     st.mark(8);
     uint32_t *rec = stage;
 #pragma unroll
@@ -1160,7 +1189,7 @@ __device__ __forceinline__ void fold_sample(const RecT *rec, const uint32_t cnt[
         const RecT *p = p0 + t;
         float e = 0.0f;
         uint32_t W = 0;
-#pragma unroll 2
+        SS_UNROLL(SS_FOLD_UNROLL)
         while (p != p0) {
             --p;
             const uint32_t r = *p;
@@ -1335,11 +1364,14 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         depth = m3.rec_n >> 16;
         rms = m3.rms;
         const RecT *rec = recs + (m3.rec_n & 0xffffu);
-        if (!(diag & 2u)) fold_sample<RecT>(rec, cnt, fk, role, acc);
-        else {
+        if (SS_PRIO_FOLD) __builtin_amdgcn_s_setprio(SS_PRIO_FOLD);
+        if (!(diag & 2u)) {
+            fold_sample<RecT>(rec, cnt, fk, role, acc);
+        } else {
 #pragma unroll
             for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b];
         }
+        if (SS_PRIO_FOLD) __builtin_amdgcn_s_setprio(0);
     } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
@@ -1416,7 +1448,10 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
 /* DIAG = true only for the profiling ablations (SS_DIAG); the production
  * instance has every ablation branch folded away. */
 template <bool DIAG>
-__global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
+#ifndef SS_MAIN_OCC
+#define SS_MAIN_OCC 4     /* waves per SIMD the main kernel is compiled for (VGPR budget) */
+#endif
+__global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(SS_MAIN_OCC)))
 void ss_score_main(ss_score_args a)
 {
     const uint32_t diag = DIAG ? a.diag : 0u;
