@@ -1218,17 +1218,25 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
 /* lanes 0..16: off_t[s..s+16], 17..32: ref[s..s+15], 33..49: off_n[s..s+16] */
 __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s)
 {
-    const uint32_t lane = lane_id();
+    /* The block's bases are wave-uniform (scalar registers); the lane offset is
+     * made opaque here so the compiler cannot hoist per-lane 64-bit pointers
+     * out of the block loop (they would stay live for the whole kernel and
+     * spill to scratch). */
+    uint32_t lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const uint32_t *ot = a.off_t + s, *on = a.off_n + s;
+    const uint8_t *rf = a.ref + s;
+    const uint64_t rem = a.n_sites - s;               /* > 0 */
     uint32_t v = 0;
     if (lane < 17u) {
-        if (s + lane <= a.n_sites) v = a.off_t[s + lane];
+        if (lane <= rem) v = ot[lane];
     } else if (lane < 33u) {
-        if (s + (lane - 17u) < a.n_sites) {
-            const uint32_t rc = a.ref[s + (lane - 17u)];
+        if (lane - 17u < rem) {
+            const uint32_t rc = rf[lane - 17u];
             v = rc | (uint32_t)ss_tab_nt16(a.m)[rc] << 8;
         }
     } else if (lane < 50u) {
-        if (s + (lane - 33u) <= a.n_sites) v = a.off_n[s + (lane - 33u)];
+        if (lane - 33u <= rem) v = on[lane - 33u];
     }
     return v;
 }
@@ -1250,8 +1258,10 @@ __device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
 {
     const uint32_t lane = lane_id();
     /* lane i (< 16): off_t[i] is desc itself, off_t[i + 1] the next lane's
-     * (DPP wave_shl:1); off_n[i] comes from lane 33 + i */
-    const uint32_t n0 = (uint32_t)__shfl((int)desc, 33 + (int)lane);
+     * (DPP wave_shl:1); off_n[i] comes from lane 33 + i: lane 32 + i by a
+     * permlane32 swap, then one more wave_shl:1 (no LDS address register) */
+    const auto sw = __builtin_amdgcn_permlane32_swap(desc, desc, false, false);
+    const uint32_t n0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sw[1], 0x130, 0xf, 0xf, false);
     const uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)desc, 0x130, 0xf, 0xf, false) - desc;
     const uint32_t nn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n0, 0x130, 0xf, 0xf, false) - n0;
     const uint32_t sz = lane < nsite ? nt + nn : 0u;
