@@ -1,13 +1,19 @@
 /* column_pileup.c -- see column_pileup.h for the rules being reproduced.
  *
- * A producer thread reads records, keeps the loaded ones in load order, and
- * whenever the finalisation frontier W has moved far enough it builds the
- * columns of the window [lo, hi) in two passes over the loaded reads:
- * difference arrays give every column's raw and packed entry counts, a prefix
- * sum gives each column's slice of the output, and a second pass scatters the
- * packed entries (load order within a column is kept because reads are
- * visited in load order).  The columns go to the consumer in chunks through
- * a small ring, as the positions of a compressed sparse row batch. */
+ * Per sample:
+ *   - a reader thread reads records, applies the keep / coverage rules and
+ *     keeps the loaded reads in load order.  Whenever the finalisation
+ *     frontier W has moved far enough it cuts the positions behind it into
+ *     windows of at most SEG_MAX positions and queues one job per window: the
+ *     window and the loaded reads that reach into it;
+ *   - worker threads build the jobs' columns, any job on any worker: pass 1
+ *     adds each read's runs to difference arrays (raw and packed entry
+ *     counts per column), a prefix sum gives every column its output slots,
+ *     pass 2 scatters the packed entries, reads in load order, so the entries
+ *     of a column keep the reference's pileup order;
+ *   - the consumer (col_stream_next) drains the jobs in window order.
+ * A read is recycled once the last job that references it has been drained.
+ * Jobs live in a ring of N_JOBS slots; the reader waits for a free slot. */
 #include "column_pileup.h"
 
 #include <pthread.h>
@@ -17,50 +23,62 @@
 
 #include "bam_reader.h"
 
-#define SEG_MIN    1024
-#define SEG_MAX    2048
-#define CHUNK_MIN  16384      /* columns per published chunk */
-#define N_CHUNKS   8
+#define SEG_MIN    1024       /* frontier advance that cuts windows */
+#define SEG_MAX    2048       /* positions per window */
+#define N_JOBS     64
+#define MAX_WORKERS 16
 
 typedef struct {
     int64_t beg, end;         /* reference span (bam_calend) */
-    int64_t from;             /* first position not yet built for this read */
+    int64_t from;             /* first position this read contributes to */
+    uint64_t last_job;        /* the last job that references it (set when retired) */
     uint32_t pk;              /* mapQ | strand << 20 */
     int single;               /* one M operation covering [beg, end) */
     bam_record_t b;
 } cread_t;
 
+enum { JOB_FREE, JOB_READY, JOB_BUSY, JOB_DONE };
+
 typedef struct {
+    int state;
+    int last;                 /* end-of-stream marker: no columns */
+    uint64_t seq;
+    int32_t tid;
+    int64_t lo, hi;
+    cread_t **reads;          /* loaded reads that reach into [lo, hi), load order */
+    int n_reads, m_reads;
     int32_t *hdr;             /* tid, pos, r, np per column */
     uint32_t *pk;
-    size_t n, cap, n_pk, cap_pk;
-    int last;                 /* the stream ends after this chunk */
-} chunk_t;
+    size_t n, cap, cap_pk;
+} job_t;
+
+typedef struct {
+    int32_t *raw, *npk;       /* difference arrays / counts, SEG_MAX + 1 */
+    uint32_t *off;
+} scratch_t;
 
 struct col_stream {
     bgzf_reader_t *fp;
     uint32_t flag_mask;
     int mapq_thresh;
-    /* producer state */
+    int error;
+    /* reader state */
     cread_t **act;            /* loaded reads, load order */
     int n_act, m_act;
+    cread_t **retired;        /* FIFO of reads whose last job is queued, by last_job */
+    size_t ret_head, ret_tail, m_ret;
     cread_t **pool;           /* recycled reads (their buffers are reused) */
     int n_pool, m_pool;
-    int32_t *raw, *npk;       /* window difference arrays / counts, SEG_MAX + 1 */
-    uint32_t *off;
-    uint32_t *wbuf;           /* the window's entries */
-    size_t cap_w;
-    int error;
-    /* ring */
-    chunk_t chunks[N_CHUNKS];
-    chunk_t *fill;
-    uint64_t produced, consumed;
-    int stop;
+    /* job ring */
+    job_t jobs[N_JOBS];
+    uint64_t queued, next_build, drained;
+    int stop, n_workers;
     pthread_mutex_t mu;
-    pthread_cond_t cv;
-    pthread_t th;
+    pthread_cond_t cv_reader, cv_work, cv_done;
+    pthread_t reader, workers[MAX_WORKERS];
+    scratch_t scr[MAX_WORKERS];
     /* consumer cursor */
-    chunk_t *cur;
+    job_t *cur;
     size_t step, pk_off;
     int ended;
 };
@@ -72,27 +90,7 @@ static void *xalloc(void *p, size_t n)
     return q;
 }
 
-/* ---- ring -------------------------------------------------------------- */
-static chunk_t *chunk_acquire(col_stream_t *S)
-{
-    pthread_mutex_lock(&S->mu);
-    while (!S->stop && S->produced - S->consumed >= N_CHUNKS) pthread_cond_wait(&S->cv, &S->mu);
-    chunk_t *c = S->stop ? NULL : &S->chunks[S->produced % N_CHUNKS];
-    pthread_mutex_unlock(&S->mu);
-    if (c) { c->n = c->n_pk = 0; c->last = 0; }
-    return c;
-}
-
-static void chunk_publish(col_stream_t *S)
-{
-    pthread_mutex_lock(&S->mu);
-    ++S->produced;
-    pthread_cond_broadcast(&S->cv);
-    pthread_mutex_unlock(&S->mu);
-    S->fill = NULL;
-}
-
-/* ---- window build ---------------------------------------------------------- */
+/* ---- window build (workers) ------------------------------------------------ */
 static void add_run(int32_t *d, int64_t a, int64_t b, int64_t lo, int64_t hi)
 {
     if (a < lo) a = lo;
@@ -112,17 +110,16 @@ static void scatter_run(uint32_t *restrict out, uint32_t *restrict off, uint32_t
     for (uint32_t i = 0; i < n; ++i) ++off[i];
 }
 
-/* Builds and publishes the columns of contig tid in [lo, hi), hi - lo <= SEG_MAX.
- * Returns 0, or -1 when the consumer has gone. */
-static int build_window(col_stream_t *S, int32_t tid, int64_t lo, int64_t hi)
+static void build_job(job_t *J, scratch_t *sc)
 {
-    const int64_t len = hi - lo;
-    int32_t *raw = S->raw, *npk = S->npk;
+    const int64_t lo = J->lo, hi = J->hi, len = hi - lo;
+    int32_t *raw = sc->raw, *npk = sc->npk;
+    uint32_t *off = sc->off;
     memset(raw, 0, sizeof(int32_t) * (size_t)(len + 1));
     memset(npk, 0, sizeof(int32_t) * (size_t)(len + 1));
     /* pass 1: entry counts per column */
-    for (int i = 0; i < S->n_act; ++i) {
-        const cread_t *r = S->act[i];
+    for (int i = 0; i < J->n_reads; ++i) {
+        const cread_t *r = J->reads[i];
         const int64_t from = r->from > lo ? r->from : lo;
         if (r->single) {
             add_run(raw, from, r->end, lo, hi);
@@ -146,7 +143,6 @@ static int build_window(col_stream_t *S, int32_t tid, int64_t lo, int64_t hi)
         }
     }
     /* prefix sums: counts, then each column's first output slot */
-    uint32_t *off = S->off;
     int32_t cr = 0, cp = 0;
     uint32_t tot = 0;
     size_t ncol = 0;
@@ -158,28 +154,20 @@ static int build_window(col_stream_t *S, int32_t tid, int64_t lo, int64_t hi)
         tot += (uint32_t)cp;
         ncol += cr > 0;
     }
-    if (ncol == 0) return 0;
-    /* the chunk receives the window */
-    if (!S->fill && !(S->fill = chunk_acquire(S))) return -1;
-    chunk_t *c = S->fill;
-    if (c->n + ncol > c->cap) {
-        c->cap = 2 * (c->n + ncol) + 4096;
-        c->hdr = (int32_t *)xalloc(c->hdr, sizeof(int32_t) * 4 * c->cap);
+    J->n = ncol;
+    if (ncol == 0) return;
+    if (ncol > J->cap) {
+        J->cap = ncol + 256;
+        J->hdr = (int32_t *)xalloc(J->hdr, sizeof(int32_t) * 4 * J->cap);
     }
-    if (c->n_pk + tot > c->cap_pk) {
-        c->cap_pk = 2 * (c->n_pk + tot) + 65536;
-        c->pk = (uint32_t *)xalloc(c->pk, sizeof(uint32_t) * c->cap_pk);
+    if (tot > J->cap_pk) {
+        J->cap_pk = tot + tot / 4 + 4096;
+        J->pk = (uint32_t *)xalloc(J->pk, sizeof(uint32_t) * J->cap_pk);
     }
-    /* the entries are scattered into a window buffer that stays in cache,
-     * then appended to the chunk sequentially */
-    if (tot > S->cap_w) {
-        S->cap_w = 2 * tot;
-        S->wbuf = (uint32_t *)xalloc(S->wbuf, sizeof(uint32_t) * S->cap_w);
-    }
-    uint32_t *out = S->wbuf;
+    uint32_t *out = J->pk;
     /* pass 2: scatter the packed entries, reads in load order */
-    for (int i = 0; i < S->n_act; ++i) {
-        const cread_t *r = S->act[i];
+    for (int i = 0; i < J->n_reads; ++i) {
+        const cread_t *r = J->reads[i];
         const int64_t from = r->from > lo ? r->from : lo;
         const uint8_t *seq = bam_rec_seq(&r->b), *qual = bam_rec_qual(&r->b);
         if (r->single) {
@@ -203,14 +191,13 @@ static int build_window(col_stream_t *S, int32_t tid, int64_t lo, int64_t hi)
             }
         }
     }
-    memcpy(c->pk + c->n_pk, out, sizeof(uint32_t) * tot);
     /* headers: off[] now holds each column's end slot */
-    int32_t *h = c->hdr + 4 * c->n;
+    int32_t *h = J->hdr;
     uint32_t beg = 0;
     for (int64_t i = 0; i < len; ++i) {
         const uint32_t e = off[i];
         if (raw[i] > 0) {
-            h[0] = tid;
+            h[0] = J->tid;
             h[1] = (int32_t)(lo + i);
             h[2] = raw[i];
             h[3] = (int32_t)(e - beg);
@@ -218,35 +205,107 @@ static int build_window(col_stream_t *S, int32_t tid, int64_t lo, int64_t hi)
         }
         beg = e;
     }
-    c->n += ncol;
-    c->n_pk += tot;
-    if (c->n >= CHUNK_MIN) chunk_publish(S);
-    return 0;
 }
 
-/* Recycles the loaded reads with nothing left at or after position lo. */
-static void purge(col_stream_t *S, int64_t lo)
+typedef struct {
+    col_stream_t *S;
+    int id;
+} worker_arg_t;
+
+static void *worker_main(void *arg)
 {
-    int k = 0;
-    for (int i = 0; i < S->n_act; ++i) {
-        cread_t *r = S->act[i];
-        if (r->end <= lo || r->from >= r->end) {
-            if (S->n_pool == S->m_pool) {
-                S->m_pool = S->m_pool ? 2 * S->m_pool : 256;
-                S->pool = (cread_t **)xalloc(S->pool, sizeof(cread_t *) * (size_t)S->m_pool);
-            }
-            S->pool[S->n_pool++] = r;
-            continue;
-        }
-        if (r->from < lo) r->from = lo;
-        S->act[k++] = r;
+    worker_arg_t *w = (worker_arg_t *)arg;
+    col_stream_t *S = w->S;
+    scratch_t *sc = &S->scr[w->id];
+    free(w);
+    pthread_mutex_lock(&S->mu);
+    for (;;) {
+        while (!S->stop && !(S->next_build < S->queued && S->jobs[S->next_build % N_JOBS].state == JOB_READY))
+            pthread_cond_wait(&S->cv_work, &S->mu);
+        if (S->stop) break;
+        job_t *J = &S->jobs[S->next_build % N_JOBS];
+        ++S->next_build;
+        J->state = JOB_BUSY;
+        pthread_mutex_unlock(&S->mu);
+        if (!J->last) build_job(J, sc);
+        pthread_mutex_lock(&S->mu);
+        J->state = JOB_DONE;
+        pthread_cond_broadcast(&S->cv_done);
     }
-    S->n_act = k;
+    pthread_mutex_unlock(&S->mu);
+    return NULL;
 }
 
-/* Builds every column of contig tid before `upto` (INT64_MAX: the whole
- * contig; *lo is then left alone, the caller starts the next contig). */
-static int build_until(col_stream_t *S, int32_t tid, int64_t *lo, int64_t upto)
+/* ---- reader -------------------------------------------------------------------- */
+static cread_t *read_new(col_stream_t *S)
+{
+    if (S->n_pool) return S->pool[--S->n_pool];
+    cread_t *r = (cread_t *)calloc(1, sizeof(cread_t));
+    if (!r) { fprintf(stderr, "out of memory\n"); exit(1); }
+    return r;
+}
+
+/* Recycles the retired reads whose last job has been drained (reader thread,
+ * mu held for `drained`). */
+static void recycle(col_stream_t *S)
+{
+    while (S->ret_head < S->ret_tail) {
+        cread_t *r = S->retired[S->ret_head % S->m_ret];
+        if (r->last_job >= S->drained) break;
+        ++S->ret_head;
+        if (S->n_pool == S->m_pool) {
+            S->m_pool = S->m_pool ? 2 * S->m_pool : 1024;
+            S->pool = (cread_t **)xalloc(S->pool, sizeof(cread_t *) * (size_t)S->m_pool);
+        }
+        S->pool[S->n_pool++] = r;
+    }
+}
+
+/* Appends r to the retired FIFO.  The FIFO and the pool belong to the reader
+ * thread (recycle() runs there too), so no lock; last_job never decreases. */
+static void retire(col_stream_t *S, cread_t *r, uint64_t last_job)
+{
+    r->last_job = last_job;
+    if (S->ret_tail - S->ret_head == S->m_ret) {           /* grow the ring, keeping FIFO order */
+        const size_t m = S->m_ret ? 2 * S->m_ret : 4096;
+        cread_t **q = (cread_t **)xalloc(NULL, sizeof(cread_t *) * m);
+        for (size_t i = S->ret_head; i < S->ret_tail; ++i) q[i - S->ret_head] = S->retired[i % S->m_ret];
+        S->ret_tail -= S->ret_head;
+        S->ret_head = 0;
+        free(S->retired);
+        S->retired = q;
+        S->m_ret = m;
+    }
+    S->retired[S->ret_tail++ % S->m_ret] = r;
+}
+
+/* Takes the next job slot (waits for the consumer to drain one), or NULL once
+ * the stream is stopped. */
+static job_t *job_acquire(col_stream_t *S)
+{
+    pthread_mutex_lock(&S->mu);
+    while (!S->stop && S->queued - S->drained >= N_JOBS) pthread_cond_wait(&S->cv_reader, &S->mu);
+    recycle(S);
+    job_t *J = S->stop ? NULL : &S->jobs[S->queued % N_JOBS];
+    const uint64_t seq = S->queued;
+    pthread_mutex_unlock(&S->mu);
+    if (J) { J->n = 0; J->n_reads = 0; J->last = 0; J->seq = seq; }
+    return J;
+}
+
+static void job_queue(col_stream_t *S, job_t *J)
+{
+    pthread_mutex_lock(&S->mu);
+    J->state = JOB_READY;
+    ++S->queued;
+    pthread_cond_broadcast(&S->cv_work);
+    pthread_mutex_unlock(&S->mu);
+}
+
+/* Queues the windows of contig tid before `upto` (INT64_MAX: the whole
+ * contig); reads with nothing after a window are retired with it.  Returns
+ * -1 once the stream is stopped. */
+static int queue_until(col_stream_t *S, int32_t tid, int64_t *lo, int64_t upto)
 {
     for (;;) {
         /* the first position any loaded read still covers, and the last */
@@ -263,31 +322,47 @@ static int build_until(col_stream_t *S, int32_t tid, int64_t *lo, int64_t upto)
             break;
         }
         const int64_t hi = stop - first > SEG_MAX ? first + SEG_MAX : stop;
-        if (build_window(S, tid, first, hi)) return -1;
+        job_t *J = job_acquire(S);
+        if (!J) return -1;
+        J->tid = tid;
+        J->lo = first;
+        J->hi = hi;
+        if (S->n_act > J->m_reads) {
+            J->m_reads = S->n_act + 1024;
+            J->reads = (cread_t **)xalloc(J->reads, sizeof(cread_t *) * (size_t)J->m_reads);
+        }
+        int k = 0;
+        for (int i = 0; i < S->n_act; ++i) {
+            cread_t *r = S->act[i];
+            const int64_t f = r->from > first ? r->from : first;
+            if (f < r->end && f < hi) J->reads[J->n_reads++] = r;
+            if (r->end <= hi || r->from >= r->end) retire(S, r, J->seq);
+            else S->act[k++] = r;
+        }
+        S->n_act = k;
         *lo = hi;
-        purge(S, hi);
+        job_queue(S, J);
         if (hi >= upto) break;
     }
-    purge(S, *lo);
+    /* reads with nothing left at or after lo (no reference span, or passed) */
+    int k = 0;
+    for (int i = 0; i < S->n_act; ++i) {
+        cread_t *r = S->act[i];
+        if (r->end <= *lo || r->from >= r->end) retire(S, r, S->queued);
+        else S->act[k++] = r;
+    }
+    S->n_act = k;
     return 0;
 }
 
-static cread_t *read_new(col_stream_t *S)
-{
-    if (S->n_pool) return S->pool[--S->n_pool];
-    cread_t *r = (cread_t *)calloc(1, sizeof(cread_t));
-    if (!r) { fprintf(stderr, "out of memory\n"); exit(1); }
-    return r;
-}
-
-static void *producer_main(void *arg)
+static void *reader_main(void *arg)
 {
     col_stream_t *S = (col_stream_t *)arg;
     bam_record_t rec;
     memset(&rec, 0, sizeof rec);
     int32_t T = 0, max_tid = -1;     /* the walk's contig */
     int64_t W = 0;                   /* the walk's position at the next load */
-    int64_t lo = 0;                  /* columns of T before lo are built */
+    int64_t lo = 0;                  /* windows of T before lo are queued */
     int rc;
     while ((rc = bam_record_read(S->fp, &rec)) > 0) {
         if ((rec.flag & S->flag_mask) || rec.mapq < S->mapq_thresh) continue;
@@ -300,7 +375,7 @@ static void *producer_main(void *arg)
         const int keep = end > W;
         int64_t from = beg > W ? beg : W;
         if (rec.tid != T) {              /* a later contig: the current one is complete */
-            if (build_until(S, T, &lo, INT64_MAX)) goto out;
+            if (queue_until(S, T, &lo, INT64_MAX)) goto out;
             T = rec.tid;
             from = beg;
             W = beg > 0 ? beg : 0;
@@ -309,6 +384,11 @@ static void *producer_main(void *arg)
             W = beg;
         }
         if (keep) {
+            if (!S->n_pool) {                           /* take back drained reads first */
+                pthread_mutex_lock(&S->mu);
+                recycle(S);
+                pthread_mutex_unlock(&S->mu);
+            }
             cread_t *r = read_new(S);
             bam_record_copy(&r->b, &rec);
             r->beg = beg;
@@ -322,31 +402,42 @@ static void *producer_main(void *arg)
             }
             S->act[S->n_act++] = r;
         }
-        if (W - lo >= SEG_MIN && build_until(S, T, &lo, W)) goto out;
+        if (W - lo >= SEG_MIN && queue_until(S, T, &lo, W)) goto out;
     }
     if (rc < 0) S->error = 1;
-    if (build_until(S, T, &lo, INT64_MAX)) goto out;
-    if (!S->fill && !(S->fill = chunk_acquire(S))) goto out;
-    S->fill->last = 1;
-    chunk_publish(S);
+    if (queue_until(S, T, &lo, INT64_MAX)) goto out;
+    job_t *J = job_acquire(S);
+    if (J) {
+        J->last = 1;
+        job_queue(S, J);
+    }
 out:
     bam_record_free(&rec);
     return NULL;
 }
 
-col_stream_t *col_stream_start(bgzf_reader_t *fp, int mask, int thresh)
+col_stream_t *col_stream_start(bgzf_reader_t *fp, int mask, int thresh, int n_workers)
 {
     col_stream_t *S = (col_stream_t *)calloc(1, sizeof *S);
     if (!S) return NULL;
     S->fp = fp;
     S->flag_mask = mask < 0 ? SS_BAM_DEF_MASK : (SS_BAM_FUNMAP | (uint32_t)mask);
     S->mapq_thresh = thresh < 0 ? 0 : thresh;
-    S->raw = (int32_t *)xalloc(NULL, sizeof(int32_t) * (SEG_MAX + 1));
-    S->npk = (int32_t *)xalloc(NULL, sizeof(int32_t) * (SEG_MAX + 1));
-    S->off = (uint32_t *)xalloc(NULL, sizeof(uint32_t) * (SEG_MAX + 1));
+    S->n_workers = n_workers < 1 ? 1 : (n_workers > MAX_WORKERS ? MAX_WORKERS : n_workers);
     pthread_mutex_init(&S->mu, NULL);
-    pthread_cond_init(&S->cv, NULL);
-    pthread_create(&S->th, NULL, producer_main, S);
+    pthread_cond_init(&S->cv_reader, NULL);
+    pthread_cond_init(&S->cv_work, NULL);
+    pthread_cond_init(&S->cv_done, NULL);
+    for (int w = 0; w < S->n_workers; ++w) {
+        S->scr[w].raw = (int32_t *)xalloc(NULL, sizeof(int32_t) * (SEG_MAX + 1));
+        S->scr[w].npk = (int32_t *)xalloc(NULL, sizeof(int32_t) * (SEG_MAX + 1));
+        S->scr[w].off = (uint32_t *)xalloc(NULL, sizeof(uint32_t) * (SEG_MAX + 1));
+        worker_arg_t *a = (worker_arg_t *)xalloc(NULL, sizeof *a);
+        a->S = S;
+        a->id = w;
+        pthread_create(&S->workers[w], NULL, worker_main, a);
+    }
+    pthread_create(&S->reader, NULL, reader_main, S);
     return S;
 }
 
@@ -355,14 +446,19 @@ int col_stream_next(col_stream_t *S, int32_t *tid, int32_t *pos, int *r, const u
     for (;;) {
         if (S->ended) return 0;
         if (S->cur && S->step < S->cur->n) break;
-        if (S->cur && S->cur->last) { S->ended = 1; return 0; }
         pthread_mutex_lock(&S->mu);
-        if (S->cur) { ++S->consumed; pthread_cond_broadcast(&S->cv); }
-        while (S->produced == S->consumed) pthread_cond_wait(&S->cv, &S->mu);
-        S->cur = &S->chunks[S->consumed % N_CHUNKS];
+        if (S->cur) {                                   /* drained: the slot goes back to the reader */
+            S->cur->state = JOB_FREE;
+            ++S->drained;
+            pthread_cond_broadcast(&S->cv_reader);
+        }
+        job_t *J = &S->jobs[S->drained % N_JOBS];
+        while (!(S->drained < S->queued && J->state == JOB_DONE)) pthread_cond_wait(&S->cv_done, &S->mu);
         pthread_mutex_unlock(&S->mu);
+        S->cur = J;
         S->step = 0;
         S->pk_off = 0;
+        if (J->last) { S->ended = 1; return 0; }
     }
     const int32_t *h = S->cur->hdr + 4 * S->step++;
     *tid = h[0];
@@ -378,22 +474,28 @@ int col_stream_stop(col_stream_t *S)
 {
     pthread_mutex_lock(&S->mu);
     S->stop = 1;
-    S->consumed = S->produced;          /* release every chunk: the producer may be waiting */
-    pthread_cond_broadcast(&S->cv);
+    pthread_cond_broadcast(&S->cv_reader);
+    pthread_cond_broadcast(&S->cv_work);
     pthread_mutex_unlock(&S->mu);
-    pthread_join(S->th, NULL);
+    pthread_join(S->reader, NULL);
+    for (int w = 0; w < S->n_workers; ++w) pthread_join(S->workers[w], NULL);
     const int err = S->error;
-    for (int c = 0; c < N_CHUNKS; ++c) { free(S->chunks[c].hdr); free(S->chunks[c].pk); }
+    for (int j = 0; j < N_JOBS; ++j) { free(S->jobs[j].reads); free(S->jobs[j].hdr); free(S->jobs[j].pk); }
+    for (int w = 0; w < S->n_workers; ++w) { free(S->scr[w].raw); free(S->scr[w].npk); free(S->scr[w].off); }
     for (int i = 0; i < S->n_act; ++i) { bam_record_free(&S->act[i]->b); free(S->act[i]); }
+    for (size_t i = S->ret_head; i < S->ret_tail; ++i) {
+        cread_t *r = S->retired[i % S->m_ret];
+        bam_record_free(&r->b);
+        free(r);
+    }
     for (int i = 0; i < S->n_pool; ++i) { bam_record_free(&S->pool[i]->b); free(S->pool[i]); }
     free(S->act);
+    free(S->retired);
     free(S->pool);
-    free(S->raw);
-    free(S->npk);
-    free(S->off);
-    free(S->wbuf);
     pthread_mutex_destroy(&S->mu);
-    pthread_cond_destroy(&S->cv);
+    pthread_cond_destroy(&S->cv_reader);
+    pthread_cond_destroy(&S->cv_work);
+    pthread_cond_destroy(&S->cv_done);
     free(S);
     return err ? -1 : 0;
 }

@@ -32,9 +32,9 @@
 
 typedef struct col_stream col_stream_t;
 
-/* Starts the producer thread over fp (header already read).  mask / thresh
- * as in dual_pileup_run. */
-col_stream_t *col_stream_start(bgzf_reader_t *fp, int mask, int thresh);
+/* Starts the reader thread over fp (header already read) and n_workers
+ * window-building threads.  mask / thresh as in dual_pileup_run. */
+col_stream_t *col_stream_start(bgzf_reader_t *fp, int mask, int thresh, int n_workers);
 /* Next reported column: 1 with its contig, position, raw entry count r and
  * the np packed non-deleted entries (valid until the next call); 0 at the
  * end of the stream. */

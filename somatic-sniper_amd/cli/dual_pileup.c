@@ -324,7 +324,9 @@ static int stream_next(stream_t *S, int32_t *tid, int32_t *pos, const uint32_t *
 static int column_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, dual_site_fn fn,
                       void *data)
 {
-    col_stream_t *a = col_stream_start(fp1, mask, thresh), *b = col_stream_start(fp2, mask, thresh);
+    const char *ew = getenv("SS_PILEUP_WORKERS");
+    const int nw = ew && *ew ? atoi(ew) : 3;                 /* window builders per sample */
+    col_stream_t *a = col_stream_start(fp1, mask, thresh, nw), *b = col_stream_start(fp2, mask, thresh, nw);
     if (!a || !b) { fprintf(stderr, "out of memory\n"); exit(1); }
     int32_t t1, p1, t2, p2;
     int r1, r2, np1, np2;
