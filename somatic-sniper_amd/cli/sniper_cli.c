@@ -106,6 +106,9 @@ typedef struct {
     pthread_cond_t cv;
     FILE *dump;
     int pileup_only;
+    /* GPU scorer creation, done on the scorer thread while the pileup runs */
+    ss_params_t prm;
+    int device;
 } run_t;
 
 static void emit_batch(run_t *R, batch_t *b)
@@ -164,6 +167,14 @@ static void emit_batch(run_t *R, batch_t *b)
 static void *scorer_main(void *arg)
 {
     run_t *R = (run_t *)arg;
+    if (!R->pileup_only) {
+        /* host tables + device upload overlap the BAM decode and pileup */
+        const int rc = ss_ctx_create(&R->prm, R->device, &R->ctx);
+        if (rc) {
+            fprintf(stderr, "[bam-somaticsniper] cannot create the GPU scorer: %s\n", ss_strerror(rc));
+            exit(1);
+        }
+    }
     pthread_mutex_lock(&R->mu);
     for (;;) {
         while (R->pending < 0 && !R->quit) pthread_cond_wait(&R->cv, &R->mu);
@@ -357,19 +368,16 @@ int main(int argc, char *argv[])
     const char *dump = getenv("SS_DUMP_PILEUP");
     if (dump && *dump) R.dump = fopen(dump, "w");
     const int pileup_only = env_int("SS_PILEUP_ONLY", 0);
-    const int rc_ctx = pileup_only ? SS_OK : ss_ctx_create(&prm, env_int("SS_DEVICE", 0), &R.ctx);
-    if (rc_ctx) {
-        fprintf(stderr, "[bam-somaticsniper] cannot create the GPU scorer: %s\n", ss_strerror(rc_ctx));
-        return 1;
-    }
-    ss_write_header(R.out, fmt, fn_fa, normal_id, tumor_id);
     const int cap = env_int("SS_BATCH", 1 << 20);
     batch_init(&R.bat[0], (size_t)(cap > 0 ? cap : 1 << 20));
     batch_init(&R.bat[1], (size_t)(cap > 0 ? cap : 1 << 20));
     pthread_mutex_init(&R.mu, NULL);
     pthread_cond_init(&R.cv, NULL);
     R.pileup_only = pileup_only;
-    pthread_create(&R.th, NULL, scorer_main, &R);
+    R.prm = prm;
+    R.device = env_int("SS_DEVICE", 0);
+    pthread_create(&R.th, NULL, scorer_main, &R);      /* creates the GPU scorer first */
+    ss_write_header(R.out, fmt, fn_fa, normal_id, tumor_id);
     dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, env_int("SS_PILEUP_THREADS", 2), on_site, &R);
     if (R.bat[R.fill].n) submit(&R);
     pthread_mutex_lock(&R.mu);
