@@ -175,8 +175,15 @@ int  ss_ctx_check(ss_ctx_t *ctx);
 
 /* Score a host batch: stages through pinned buffers, H2D, kernel, D2H, sorts
  * the emitted calls by site.  out->score / calls / glf are host pointers,
- * out->n_calls a host u32.  Synchronous. */
+ * out->n_calls a host u32.  Synchronous.  Input arrays that live in memory
+ * from ss_host_alloc are copied to the device straight from there (no
+ * staging copy). */
 int  ss_score_batch_host(ss_ctx_t *ctx, const ss_batch_t *batch, const ss_out_t *out);
+
+/* Page-locked host memory for batch arrays (callers that build batches in
+ * place, e.g. the CLI's pileup loop); NULL on failure.  No context needed. */
+void *ss_host_alloc(size_t bytes);
+void  ss_host_free(void *p);
 
 /* Host table inspection (for parity tests): FNV-1a-64 over the raw
  * little-endian doubles of fk[256], coef[64*256*256], lhet[256*256]; q_r. */

@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "ss_score_batch_device", "ss_score_batch_host", "ss_ctx_check", "ss_table_hashes",
     "ss_table_copy", "ss_synth_default", "ss_synth_batch_host", "ss_synth_batch_device",
     "ss_set_kernel_timing", "ss_last_kernel_ms", "ss_kernel_time_log", "ss_model_check", "ss_model_pinned",
+    "ss_host_alloc", "ss_host_free",
 )
 
 
@@ -164,6 +165,25 @@ class Batch:
         return Batch(*(np.ascontiguousarray(a) for a in (self.ref, self.off_tumor, self.off_normal,
                                                             self.reads_tumor, self.reads_normal)))
 
+    def pinned(self) -> "Batch":
+        """A copy whose arrays live in page-locked memory from ss_host_alloc
+        (ss_score_batch_host then copies them to the device without staging).
+        The memory is freed when the returned arrays are garbage-collected."""
+        import weakref
+        lib = load_library()
+        out = []
+        for a in (self.ref, self.off_tumor, self.off_normal, self.reads_tumor, self.reads_normal):
+            nbytes = max(1, a.nbytes)
+            p = lib.ss_host_alloc(nbytes)
+            if not p:
+                raise MemoryError("ss_host_alloc failed")
+            buf = (C.c_char * nbytes).from_address(p)
+            v = np.frombuffer(buf, dtype=a.dtype, count=a.size)
+            v[...] = a
+            weakref.finalize(buf, lib.ss_host_free, p)
+            out.append(v)
+        return Batch(*out)
+
     def algorithmic_bytes(self) -> int:
         """4 B per packed read + 16 B per site."""
         return 4 * (int(self.off_tumor[-1]) + int(self.off_normal[-1])) + 16 * self.n_sites
@@ -205,6 +225,9 @@ def load_library():
     lib.ss_ctx_destroy.argtypes = [vp]
     lib.ss_score_batch_device.argtypes = [vp, vp, vp, vp]
     lib.ss_score_batch_host.argtypes = [vp, vp, vp]
+    lib.ss_host_alloc.restype = vp
+    lib.ss_host_alloc.argtypes = [C.c_size_t]
+    lib.ss_host_free.argtypes = [vp]
     lib.ss_ctx_check.argtypes = [vp]
     lib.ss_table_hashes.argtypes = [vp, vp, vp, vp, vp]
     lib.ss_table_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp]

@@ -19,14 +19,16 @@
  *
  * Environment: SS_DEVICE (GPU index, default 0), SS_BATCH (sites per batch,
  * default 2^20), SS_BGZF_THREADS (inflate threads per BAM, default 4),
- * SS_PILEUP_THREADS (2, default: column pileup, one thread per sample;
+ * SS_PILEUP_THREADS (2, default: column pileup, per sample a reader thread and
+ * SS_PILEUP_WORKERS (default 3) window builders;
  * 1: tumor and normal walks on their own threads; 0: one thread),
  * SS_DUMP_PILEUP=FILE (test hook: also write every reported site, see
  * dump_site()), SS_PILEUP_ONLY=1 (test / timing hook: walk (and dump) without
  * scoring, so the pileup restatement is testable on a host without a GPU; no
- * output records are written).
+ * output records are written), SS_TIMING=1 (phase times on stderr).
  */
 #include <getopt.h>
+#include <time.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -164,12 +166,27 @@ static void emit_batch(run_t *R, batch_t *b)
     }
 }
 
+/* SS_TIMING=1: phase times on stderr (seconds since start) */
+static double t_start;
+static int timing;
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+static void stamp(const char *what)
+{
+    if (timing) fprintf(stderr, "[timing] %-24s %.3f s\n", what, now_s() - t_start);
+}
+
 static void *scorer_main(void *arg)
 {
     run_t *R = (run_t *)arg;
     if (!R->pileup_only) {
         /* host tables + device upload overlap the BAM decode and pileup */
         const int rc = ss_ctx_create(&R->prm, R->device, &R->ctx);
+        stamp("scorer ready");
         if (rc) {
             fprintf(stderr, "[bam-somaticsniper] cannot create the GPU scorer: %s\n", ss_strerror(rc));
             exit(1);
@@ -182,6 +199,7 @@ static void *scorer_main(void *arg)
         batch_t *b = &R->bat[R->pending];
         pthread_mutex_unlock(&R->mu);
         if (!R->failed) emit_batch(R, b);
+        stamp("batch scored");
         b->n = b->nt = b->nn = 0;
         pthread_mutex_lock(&R->mu);
         R->pending = -1;
@@ -296,6 +314,8 @@ static int env_int(const char *name, int dflt)
 
 int main(int argc, char *argv[])
 {
+    t_start = now_s();
+    timing = getenv("SS_TIMING") != NULL;
     ss_params_t prm;
     ss_params_default(&prm);
     const char *normal_id = "NORMAL", *tumor_id = "TUMOR", *fn_fa = NULL, *fmt_name = "classic";
@@ -379,6 +399,7 @@ int main(int argc, char *argv[])
     pthread_create(&R.th, NULL, scorer_main, &R);      /* creates the GPU scorer first */
     ss_write_header(R.out, fmt, fn_fa, normal_id, tumor_id);
     dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, env_int("SS_PILEUP_THREADS", 2), on_site, &R);
+    stamp("pileup done");
     if (R.bat[R.fill].n) submit(&R);
     pthread_mutex_lock(&R.mu);
     R.quit = 1;
@@ -393,8 +414,10 @@ int main(int argc, char *argv[])
     free(R.cur_ref);
     batch_free(&R.bat[0]);
     batch_free(&R.bat[1]);
+    stamp("output written");
     if (R.ctx) ss_ctx_destroy(R.ctx);
     if (R.dump) fclose(R.dump);
     fclose(R.out);
+    stamp("exit");
     return R.failed ? 1 : 0;
 }

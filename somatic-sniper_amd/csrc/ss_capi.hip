@@ -347,6 +347,30 @@ static int ensure_stage(ss_ctx_t *c, size_t bytes)
     return SS_OK;
 }
 
+extern "C" void *ss_host_alloc(size_t bytes)
+{
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+extern "C" void ss_host_free(void *p)
+{
+    if (p) hipHostFree(p);
+}
+
+/* is [p, p + n) page-locked host memory the device can read directly? */
+static bool pinned_host(const void *p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();               /* plain pageable memory: not an error */
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 extern "C" int ss_score_batch_host(ss_ctx_t *c, const ss_batch_t *b, const ss_out_t *o)
 {
     if (!c || !b || !o || !o->score) return SS_E_INVAL;
@@ -363,7 +387,6 @@ extern "C" int ss_score_batch_host(ss_ctx_t *c, const ss_batch_t *b, const ss_ou
     const size_t o_on = off;    off = align_up(off + 4 * (n + 1));
     const size_t o_rt = off;    off = align_up(off + 4 * nt);
     const size_t o_rn = off;    off = align_up(off + 4 * nn);
-    const size_t in_bytes = off;
     const size_t o_sc = off;    off = align_up(off + 4 * n);
     const size_t o_cnt = off;   off = align_up(off + 16);
     const size_t o_calls = off; off = align_up(off + sizeof(ss_call_t) * (size_t)cap);
@@ -373,13 +396,21 @@ extern "C" int ss_score_batch_host(ss_ctx_t *c, const ss_batch_t *b, const ss_ou
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
     char *h = (char *)c->h_stage, *d = (char *)c->d_stage;
-    memcpy(h + o_ref, b->ref, n);
-    memcpy(h + o_ot, b->off_tumor, 4 * (n + 1));
-    memcpy(h + o_on, b->off_normal, 4 * (n + 1));
-    if (nt) memcpy(h + o_rt, b->reads_tumor, 4 * nt);
-    if (nn) memcpy(h + o_rn, b->reads_normal, 4 * nn);
     hipStream_t s = c->hstream;
-    HIPCHK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s));
+    /* inputs already in page-locked memory go to the device directly; the
+     * rest through the pinned staging area, one H2D for all of them */
+    const struct { const void *src; size_t off, bytes; } in[5] = {
+        {b->ref, o_ref, n}, {b->off_tumor, o_ot, 4 * (n + 1)}, {b->off_normal, o_on, 4 * (n + 1)},
+        {b->reads_tumor, o_rt, 4 * nt}, {b->reads_normal, o_rn, 4 * nn}};
+    for (int k = 0; k < 5; ++k) {
+        if (!in[k].bytes) continue;
+        const void *src = in[k].src;
+        if (!pinned_host(src)) {
+            memcpy(h + in[k].off, src, in[k].bytes);
+            src = h + in[k].off;
+        }
+        HIPCHK(hipMemcpyAsync(d + in[k].off, src, in[k].bytes, hipMemcpyHostToDevice, s));
+    }
     ss_batch_t db = {n, (const uint8_t *)(d + o_ref), (const uint32_t *)(d + o_ot),
                      (const uint32_t *)(d + o_on), (const uint32_t *)(d + o_rt),
                      (const uint32_t *)(d + o_rn)};

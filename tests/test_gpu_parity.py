@@ -91,6 +91,19 @@ def test_kernel_routing_mix(pkg, oracle, ctx):
     ctx.check()
 
 
+def test_pinned_host_batch(pkg, oracle, ctx):
+    """Inputs in ss_host_alloc memory take the no-staging H2D path of
+    ss_score_batch_host: same results as pageable inputs and the oracle."""
+    b = pkg.synth_batch_host(pkg.Synth.default(60, 30, **EXOTIC), 5, 3000)
+    p = b.pinned()
+    assert (p.reads_tumor == b.reads_tumor).all() and (p.off_normal == b.off_normal).all()
+    s1, c1, g1 = ctx.score_batch(b, want_glf=True)
+    s2, c2, g2 = ctx.score_batch(p, want_glf=True)
+    assert (s1 == s2).all() and (g1.view(np.uint8) == g2.view(np.uint8)).all()
+    assert (c1.view(np.uint8) == c2.view(np.uint8)).all()
+    assert_parity(pkg, oracle, p, ctx=ctx)
+
+
 def test_giant_parity(pkg, oracle, ctx):
     """> 4096 reads in a sample -> giant kernel with global scratch."""
     big = pkg.synth_batch_host(pkg.Synth.default(6000, 4500, fixed_depth=1, **EXOTIC), 0, 6)

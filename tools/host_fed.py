@@ -19,12 +19,15 @@ def main():
     ap.add_argument("--lt", type=float, default=60)
     ap.add_argument("--ln", type=float, default=30)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--pinned", action="store_true", help="inputs in ss_host_alloc memory (no staging copy)")
     args = ap.parse_args()
     from __graft_entry__ import load_package
     pkg = load_package()
     t0 = time.perf_counter()
     b = pkg.synth_batch_host(pkg.Synth.default(args.lt, args.ln), 0, args.sites)
     gen_s = time.perf_counter() - t0
+    if args.pinned:
+        b = b.pinned()
     ctx = pkg.Context()
     ctx.score_batch(b)                       # warm-up (allocations, first launch)
     times = []
@@ -35,7 +38,8 @@ def main():
     best, mean = min(times), sum(times) / len(times)
     nbytes = b.ref.nbytes + b.off_tumor.nbytes + b.off_normal.nbytes + b.reads_tumor.nbytes + \
         b.reads_normal.nbytes
-    print(json.dumps({"path": "ss_score_batch_host (PCIe-inclusive)", "sites": args.sites,
+    print(json.dumps({"path": "ss_score_batch_host (PCIe-inclusive)", "pinned_inputs": args.pinned,
+                      "sites": args.sites,
                       "lt": args.lt, "ln": args.ln, "input_bytes": nbytes,
                       "sites_per_s_best": round(args.sites / best, 1),
                       "sites_per_s_mean": round(args.sites / mean, 1),
