@@ -210,12 +210,19 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     if (o->calls && !o->n_calls) return SS_E_INVAL;
     HIPCHK(hipSetDevice(c->device));
     /* main kernel: 4 waves per workgroup, one 16-site block per wave per
-     * iteration, grid-strided; 4 workgroups fit a CU (LDS), so 16 per CU gives
-     * each CU four rounds of waves for load balance.  Each wave owns a deep-list
+     * iteration, grid-strided; 4 workgroups fit a CU (LDS).  128 per CU gives
+     * each CU 32 rounds of short-lived waves: the dispatcher's refill balances
+     * the load and keeps co-resident waves in different phases (sort / fold /
+     * gathers) -- measured +5.5% over 4 rounds.  Each wave owns a deep-list
      * segment as long as the most blocks it can visit, times 16 sites. */
     const uint64_t site_blocks = (b->n_sites + 15) / 16;
     uint64_t blocks = (site_blocks + 3) / 4;
-    const uint64_t max_blocks = (uint64_t)c->n_cu * SS_MAIN_GRID_PER_CU;
+    uint64_t per_cu = SS_MAIN_GRID_DEFAULT;
+    {   /* tuning experiments: workgroups per CU (d_deep_seg is sized for SS_MAIN_GRID_PER_CU) */
+        const char *g = getenv("SS_MAIN_GRID");
+        if (g && atoi(g) > 0 && atoi(g) <= SS_MAIN_GRID_PER_CU) per_cu = (uint64_t)atoi(g);
+    }
+    const uint64_t max_blocks = (uint64_t)c->n_cu * per_cu;
     if (blocks > max_blocks) blocks = max_blocks;
     const uint64_t nseg = blocks * (SS_MAIN_BLOCK / 64);
     const uint64_t seg_cap = (site_blocks + nseg - 1) / nseg * 16;

@@ -86,7 +86,8 @@ struct ss_score_args {
 
 /* Launch geometry constants shared with the host. */
 #define SS_MAIN_BLOCK      256   /* 4 waves                                    */
-#define SS_MAIN_GRID_PER_CU 16   /* main-kernel workgroups per CU at most      */
+#define SS_MAIN_GRID_PER_CU 256  /* main-kernel workgroups per CU at most (deep-list segments) */
+#define SS_MAIN_GRID_DEFAULT 128 /* ... and by default: 4 resident, 32 rounds of short-lived waves (A/B: +5.5% over 16) */
 #define SS_MAIN_MAXN       256   /* per-sample depth handled by the main kernel */
 #define SS_DEEP_BLOCK      256
 #define SS_DEEP_MAXN       4096  /* per-sample depth sorted in LDS by the deep kernel */
