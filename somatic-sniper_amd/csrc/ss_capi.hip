@@ -141,7 +141,7 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
             }
     }
     TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t)));
-    TRY(dev_alloc((void **)&c->d_deep_seg, (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t)));
+    TRY(dev_alloc((void **)&c->d_deep_seg, (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * 4 * sizeof(uint32_t)));
     c->giant_cap = 1u << 16;
     TRY(dev_alloc((void **)&c->d_giant_list, c->giant_cap * sizeof(uint32_t)));
     c->giant_keys = 1u << 20;
@@ -216,11 +216,12 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
      * gathers) -- measured +5.5% over 4 rounds.  Each wave owns a deep-list
      * segment as long as the most blocks it can visit, times 16 sites. */
     const uint64_t site_blocks = (b->n_sites + 15) / 16;
-    uint64_t blocks = (site_blocks + 3) / 4;
-    uint64_t per_cu = SS_MAIN_GRID_DEFAULT;
+    const uint64_t wpb = SS_MAIN_BLOCK / 64;              /* waves per workgroup */
+    uint64_t blocks = (site_blocks + wpb - 1) / wpb;
+    uint64_t per_cu = SS_MAIN_GRID_DEFAULT * 4 / wpb;     /* same waves per CU for any block size */
     {   /* tuning experiments: workgroups per CU (d_deep_seg is sized for SS_MAIN_GRID_PER_CU) */
         const char *g = getenv("SS_MAIN_GRID");
-        if (g && atoi(g) > 0 && atoi(g) <= SS_MAIN_GRID_PER_CU) per_cu = (uint64_t)atoi(g);
+        if (g && atoi(g) > 0 && (uint64_t)atoi(g) * wpb <= SS_MAIN_GRID_PER_CU * 4) per_cu = (uint64_t)atoi(g);
     }
     const uint64_t max_blocks = (uint64_t)c->n_cu * per_cu;
     if (blocks > max_blocks) blocks = max_blocks;

@@ -85,7 +85,9 @@ struct ss_score_args {
 #define SS_KERR_TOO_DEEP       4u
 
 /* Launch geometry constants shared with the host. */
+#ifndef SS_MAIN_BLOCK
 #define SS_MAIN_BLOCK      256   /* 4 waves                                    */
+#endif
 #define SS_MAIN_GRID_PER_CU 256  /* main-kernel workgroups per CU at most (deep-list segments) */
 #define SS_MAIN_GRID_DEFAULT 128 /* ... and by default: 4 resident, 32 rounds of short-lived waves (A/B: +5.5% over 16) */
 #define SS_MAIN_MAXN       256   /* per-sample depth handled by the main kernel */

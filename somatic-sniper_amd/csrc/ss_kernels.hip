@@ -622,11 +622,11 @@ struct Slot3 {
 
 
 struct MainLds {
-    uint32_t stage[4][STG];
-    Slot3    slot[4][2 * GB];
-    SlotRes  res[4][2 * GB];
-    uint32_t site[4][GB];
-    uint32_t refc[4][GB];
+    uint32_t stage[SS_MAIN_BLOCK / 64][STG];
+    Slot3    slot[SS_MAIN_BLOCK / 64][2 * GB];
+    SlotRes  res[SS_MAIN_BLOCK / 64][2 * GB];
+    uint32_t site[SS_MAIN_BLOCK / 64][GB];
+    uint32_t refc[SS_MAIN_BLOCK / 64][GB];
 };
 
 /* 16-bit order key (see the section comment); 0xffff = no contribution.
