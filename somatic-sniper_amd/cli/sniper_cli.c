@@ -89,6 +89,11 @@ static void batch_free(batch_t *b)
 }
 
 /* ---- run state --------------------------------------------------------- */
+/* batch ring: the pileup fills one while up to N_BATCH-1 wait for or are in
+ * the scorer, so the pileup runs ahead while the GPU scorer is still being
+ * created and never waits for one batch's scoring */
+#define N_BATCH 4
+
 typedef struct {
     /* reference */
     fasta_index_t *fai;
@@ -99,9 +104,9 @@ typedef struct {
     ss_ctx_t *ctx;
     FILE *out;
     int fmt;
-    batch_t bat[2];
+    batch_t bat[N_BATCH];
     int fill;                 /* batch being filled by the pileup thread */
-    int pending;              /* batch index handed to the scorer, -1 none */
+    int n_full;               /* filled batches queued for the scorer: fill-n_full .. fill-1 */
     int quit, failed;
     pthread_t th;
     pthread_mutex_t mu;
@@ -194,28 +199,28 @@ static void *scorer_main(void *arg)
     }
     pthread_mutex_lock(&R->mu);
     for (;;) {
-        while (R->pending < 0 && !R->quit) pthread_cond_wait(&R->cv, &R->mu);
-        if (R->pending < 0 && R->quit) break;
-        batch_t *b = &R->bat[R->pending];
+        while (R->n_full == 0 && !R->quit) pthread_cond_wait(&R->cv, &R->mu);
+        if (R->n_full == 0 && R->quit) break;
+        batch_t *b = &R->bat[(R->fill + N_BATCH - R->n_full) % N_BATCH];   /* oldest queued */
         pthread_mutex_unlock(&R->mu);
         if (!R->failed) emit_batch(R, b);
         stamp("batch scored");
         b->n = b->nt = b->nn = 0;
         pthread_mutex_lock(&R->mu);
-        R->pending = -1;
+        --R->n_full;
         pthread_cond_broadcast(&R->cv);
     }
     pthread_mutex_unlock(&R->mu);
     return NULL;
 }
 
-/* hand the filled batch to the scorer; continue in the other buffer */
+/* queue the filled batch for the scorer (in order); continue in the next free one */
 static void submit(run_t *R)
 {
     pthread_mutex_lock(&R->mu);
-    while (R->pending >= 0) pthread_cond_wait(&R->cv, &R->mu);
-    R->pending = R->fill;
-    R->fill ^= 1;
+    while (R->n_full == N_BATCH - 1) pthread_cond_wait(&R->cv, &R->mu);
+    ++R->n_full;
+    R->fill = (R->fill + 1) % N_BATCH;
     pthread_cond_broadcast(&R->cv);
     pthread_mutex_unlock(&R->mu);
 }
@@ -348,7 +353,6 @@ int main(int argc, char *argv[])
     run_t R;
     memset(&R, 0, sizeof R);
     R.cur_tid = -1;
-    R.pending = -1;
     if (fn_fa) R.fai = fasta_index_load(fn_fa);
     else {
         fprintf(stderr, "You MUST specify a reference sequence. It isn't optional.\n");
@@ -389,8 +393,7 @@ int main(int argc, char *argv[])
     if (dump && *dump) R.dump = fopen(dump, "w");
     const int pileup_only = env_int("SS_PILEUP_ONLY", 0);
     const int cap = env_int("SS_BATCH", 1 << 20);
-    batch_init(&R.bat[0], (size_t)(cap > 0 ? cap : 1 << 20));
-    batch_init(&R.bat[1], (size_t)(cap > 0 ? cap : 1 << 20));
+    for (int k = 0; k < N_BATCH; ++k) batch_init(&R.bat[k], (size_t)(cap > 0 ? cap : 1 << 20));
     pthread_mutex_init(&R.mu, NULL);
     pthread_cond_init(&R.cv, NULL);
     R.pileup_only = pileup_only;
@@ -412,8 +415,7 @@ int main(int argc, char *argv[])
     bam_header_free(&h2);
     fasta_index_free(R.fai);
     free(R.cur_ref);
-    batch_free(&R.bat[0]);
-    batch_free(&R.bat[1]);
+    for (int k = 0; k < N_BATCH; ++k) batch_free(&R.bat[k]);
     stamp("output written");
     if (R.ctx) ss_ctx_destroy(R.ctx);
     if (R.dump) fclose(R.dump);
