@@ -287,7 +287,12 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         e1 = (*c->ev)[2 * c->n_logged + 1];
         ++c->n_logged;
     }
-    int e = ss_launch_score(a, (int)blocks, c->n_cu, deep_grid, s, e0, e1);
+    int wide_grid = c->n_cu;                      /* one 8-wave workgroup per CU fits (LDS) */
+    {   /* tuning experiments: rounds of wide workgroups per CU */
+        const char *g = getenv("SS_WIDE_GRID");
+        if (g && atoi(g) > 0 && atoi(g) <= 64) wide_grid = c->n_cu * atoi(g);
+    }
+    int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, s, e0, e1);
     return e == 0 ? SS_OK : SS_E_HIP;
 }
 
