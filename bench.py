@@ -12,10 +12,11 @@ genome shard (synth shard = rank) -- no collective on the data path, weak
 scaling.  value = sites scored by all ranks / max rank time.
 
 Extra fields: "roofline" (main kernel, HIP events over the timed region,
-algorithmic bytes 4 B/read + 16 B/site) and "cpu_baseline" (the real reference
+algorithmic bytes 4 B/read + 16 B/site), "cpu_baseline" (the real reference
 glf_somatic compiled from source, oracle/_ref/ref_harness, 1 core, rank 0 at
 N=1 only, on a bounded sample of the same synthetic workload, also used as a
-parity spot check).
+parity spot check) and "cpu_baseline_all_cores" (the same on every core we may
+use, one process per core).
 """
 from __future__ import annotations
 
@@ -68,6 +69,30 @@ def cpu_baseline(lt, ln, sample, seed, gpu_scores_prefix):
         parity = bool((gpu_scores_prefix[:sample] == cpu_scores).all())
     return {"value": round(value, 1), "unit": "sites/s", "cores": 1, "kind": kind,
             "sample": desc, "parity_vs_gpu": parity}
+
+
+def cpu_baseline_all_cores(lt, ln, seed, per_proc=500_000):
+    """The reference glf_somatic on every host core we may use: one harness
+    process per core, each on its own synthetic shard (same distribution),
+    run concurrently; sites of all processes / the longest process's scoring
+    time.  None without the compiled reference."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    procs = [subprocess.Popen([harness, "synth", str(lt), str(ln), str(per_proc), "--seed", str(seed),
+                               "--shard", str(100 + k)], stdout=subprocess.PIPE, text=True)
+             for k in range(cores)]
+    secs = []
+    for p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            return None
+        secs.append(json.loads(out.strip().splitlines()[-1])["seconds"])
+    return {"value": round(cores * per_proc / max(secs), 1), "unit": "sites/s", "cores": cores,
+            "kind": "reference",
+            "sample": f"{cores} concurrent processes x {per_proc} synthetic sites ({lt}xT/{ln}xN, own shard each), "
+                      f"reference glf_somatic only, total sites / longest process time"}
 
 
 def main():
@@ -204,6 +229,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         pre = score[0][: args.cpu_sample].cpu().numpy() if S >= args.cpu_sample else None
         result["cpu_baseline"] = cpu_baseline(args.lt, args.ln, min(args.cpu_sample, S), args.seed, pre)
+        allc = cpu_baseline_all_cores(args.lt, args.ln, args.seed)
+        if allc:
+            result["cpu_baseline_all_cores"] = allc
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
