@@ -286,6 +286,10 @@ __device__ __forceinline__ float geno_p(int j, int k, const float es[4], const f
     const double lh = hom ? 0.0 : -4.343 * ss_tab_lhet(m)[c[j] << 8 | c[k]];
     float v;
     if (c2) {
+        /* the reference's layout, kept on the device: rescaled counts can sum
+         * to 256, and tot = 256 then reads row q + 1, n = 0 exactly as the
+         * reference does (a transposed, q-minor copy measured no faster and
+         * broke that aliasing) */
         const double cf = ss_tab_coef(m)[(uint32_t)clamp_bar_e(e, f) << 16 | tot << 8 | c2];
         v = hom ? (float)((double)e + cf) : (float)((lh + (double)e) + cf);
     } else {
