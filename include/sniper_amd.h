@@ -169,8 +169,10 @@ int  ss_score_batch_device(ss_ctx_t *ctx, const ss_batch_t *batch,
                            const ss_out_t *out, void *stream);
 
 /* Wait for the context's outstanding work and report sticky device-side
- * errors: SS_E_CAPACITY if a work list overflowed or a site exceeded the giant
- * scratch (such sites carry score -2).  Clears the sticky bits. */
+ * errors: SS_E_INVAL if a batch had decreasing read offsets, else
+ * SS_E_CAPACITY if a work list overflowed or a site exceeded the giant scratch
+ * (such sites carry score -2; so does a site whose offsets decrease -- the
+ * kernels never read reads for it).  Clears the sticky bits. */
 int  ss_ctx_check(ss_ctx_t *ctx);
 
 /* Score a host batch: stages through pinned buffers, H2D, kernel, D2H, sorts

@@ -338,7 +338,7 @@ extern "C" int ss_ctx_check(ss_ctx_t *c)
     HIPCHK(hipMemcpy(&err, c->d_counters + 2, sizeof(err), hipMemcpyDeviceToHost));
     if (err) {
         HIPCHK(hipMemset(c->d_counters + 2, 0, sizeof(uint32_t)));
-        return SS_E_CAPACITY;
+        return (err & SS_KERR_MALFORMED) ? SS_E_INVAL : SS_E_CAPACITY;
     }
     return SS_OK;
 }

@@ -83,6 +83,7 @@ struct ss_score_args {
 #define SS_KERR_DEEP_OVERFLOW  1u
 #define SS_KERR_GIANT_OVERFLOW 2u
 #define SS_KERR_TOO_DEEP       4u
+#define SS_KERR_MALFORMED      8u   /* decreasing read offsets: the site was not scored */
 
 /* Launch geometry constants shared with the host. */
 #ifndef SS_MAIN_BLOCK

@@ -1270,7 +1270,9 @@ __device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
     const uint32_t nn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n0, 0x130, 0xf, 0xf, false) - n0;
     const uint32_t sz = lane < nsite ? nt + nn : 0u;
     BlockScan r;
-    r.deep = __ballot(lane < nsite && sz + (nt & 1u) > PK_MAX);
+    /* a decreasing offset (malformed batch) wraps one count to ~2^32: the
+     * per-sample test keeps such a site off the packed path whatever the sum */
+    r.deep = __ballot(lane < nsite && (sz + (nt & 1u) > PK_MAX || max(nt, nn) > PK_MAX));
     int x = (int)sz;
     x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);    /* row_shr:1 */
     x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);    /* row_shr:2 */
@@ -1624,10 +1626,12 @@ struct WideLds {
 struct WideSite {
     uint32_t ot, nt, on, nn;
     bool split;        /* split placement (see split_fits): top level skipped */
+    bool over;         /* more than SS_WIDE_MAXSLOTS slots (or a wrapped count): deep kernel */
 };
 
 __device__ __forceinline__ void wide_place(WideSite &w)
 {
+    w.over = max(w.nt, w.nn) > SS_WIDE_MAXSLOTS || w.nt + (w.nt & 1u) + w.nn > SS_WIDE_MAXSLOTS;
     const bool k8 = w.nt + (w.nt & 1u) + w.nn <= 1024u;      /* the network sort_site_wide picks */
     w.split = SS_SPLIT_WIDE != 0 && (k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn));
 }
@@ -1643,7 +1647,7 @@ __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite
         const bool tum = w.split ? lane < 32u : e0 < ntr;
         const uint32_t i0 = w.split ? es : (tum ? e0 : e0 - ntr);
         const uint32_t *src = tum ? a.reads_t + w.ot + i0 : a.reads_n + w.on + i0;
-        const uint32_t lim = tum ? w.nt : w.nn;
+        const uint32_t lim = w.over ? 0u : (tum ? w.nt : w.nn);   /* nothing is loaded for an over site */
         rd[2 * r] = i0 < lim ? __builtin_nontemporal_load(src) : 0u;
         rd[2 * r + 1] = i0 + 1u < lim ? __builtin_nontemporal_load(src + 1) : 0u;
     }
@@ -1726,7 +1730,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
         const uint32_t nlist = scount - first < GB ? scount - first : GB;
         /* site i's reads are in flight while site i-1 is sorted */
         uint32_t i = 0, s_cur = 0;
-        WideSite w_cur = {0, 0, 0, 0, false};
+        WideSite w_cur = {0, 0, 0, 0, false, false};
         uint32_t rd[32];
         auto describe = [&](uint32_t k, uint32_t &s, WideSite &w) {
             s = list[first + k];
@@ -1747,7 +1751,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 const uint32_t s = s_cur;
                 const WideSite w = w_cur;
                 const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
-                if (used + slots > WIDE_ARENA && slots <= SS_WIDE_MAXSLOTS) break;   /* next sub-group */
+                if (used + slots > WIDE_ARENA && !w.over) break;   /* next sub-group */
                 uint32_t cur[32];
 #pragma unroll
                 for (int k = 0; k < 32; ++k) cur[k] = rd[k];
@@ -1756,7 +1760,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                     wide_load(a, w_cur, rd);
                 }
                 ++i;
-                if (slots > SS_WIDE_MAXSLOTS) {
+                if (w.over) {
                     if (lane == 0) {
                         const uint32_t d = atomicAdd(a.deep2_count, 1u);
                         if (d < a.deep_cap) a.deep2_list[d] = s;
@@ -1886,7 +1890,8 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
                     if (d < a.giant_cap) a.giant_list[d] = s;
                     else atomicOr(a.err, SS_KERR_GIANT_OVERFLOW);
                 } else {
-                    atomicOr(a.err, SS_KERR_TOO_DEEP);
+                    /* a count >= 2^31 can only come from decreasing offsets */
+                    atomicOr(a.err, ((nt | nn) & 0x80000000u) ? SS_KERR_MALFORMED : SS_KERR_TOO_DEEP);
                     a.score[s] = -2;
                 }
             }

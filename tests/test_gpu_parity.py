@@ -104,6 +104,30 @@ def test_pinned_host_batch(pkg, oracle, ctx):
     assert_parity(pkg, oracle, p, ctx=ctx)
 
 
+def test_malformed_offsets_reported(pkg, oracle, ctx):
+    """Decreasing read offsets (a malformed batch) wrap a site's read count to
+    ~2^32.  No kernel may read reads for such a site: it is routed through the
+    deep lists to the giant kernel, which scores it -2 without touching its
+    reads, and ss_ctx_check reports SS_E_INVAL.  Cases: a tumor count of -1
+    (odd: count + pad wraps to a small slot total, the main kernel's trap) and
+    a normal count of -7 next to a wide site.  The context stays usable."""
+    b = pkg.synth_batch_host(pkg.Synth.default(60, 30, **EXOTIC), 11, 300)
+    wide = pkg.synth_batch_host(pkg.Synth.default(700, 600, fixed_depth=1, **EXOTIC), 3, 4)
+    sites = [b.site(i) for i in range(b.n_sites)]
+    sites[200:200] = [wide.site(i) for i in range(wide.n_sites)]
+    good = pkg.Batch.from_sites(sites)
+    ot, on = good.off_tumor.copy(), good.off_normal.copy()
+    assert ot[5] >= 1 and on[202] >= 7
+    ot[6] = ot[5] - 1
+    on[203] = on[202] - 7
+    bad = pkg.Batch(good.ref, ot, on, good.reads_tumor, good.reads_normal)
+    with pytest.raises(pkg.SniperError) as ei:
+        ctx.score_batch(bad)
+    assert ei.value.code == pkg.SS_E_INVAL
+    ctx.check()                                   # the sticky bit was cleared
+    assert_parity(pkg, oracle, good, ctx=ctx)
+
+
 def test_giant_parity(pkg, oracle, ctx):
     """> 4096 reads in a sample -> giant kernel with global scratch."""
     big = pkg.synth_batch_host(pkg.Synth.default(6000, 4500, fixed_depth=1, **EXOTIC), 0, 6)
