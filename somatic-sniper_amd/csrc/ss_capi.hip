@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "sniper_amd.h"
@@ -373,6 +374,34 @@ extern "C" void ss_host_free(void *p)
 }
 
 /* is [p, p + n) page-locked host memory the device can read directly? */
+/* Pageable input -> pinned staging -> device, in pieces: each piece is copied
+ * into the staging area by SS_COPY_THREADS threads (default 8) and its H2D is
+ * queued at once, so the DMA of one piece runs while the next is copied. */
+static int copy_threads()
+{
+    const char *e = getenv("SS_COPY_THREADS");
+    const int t = e && *e ? atoi(e) : 4;
+    return t < 1 ? 1 : (t > 64 ? 64 : t);
+}
+
+static void par_memcpy(char *dst, const char *src, size_t n, int nthreads)
+{
+    const size_t min_share = (size_t)4 << 20;
+    int t = (int)std::min<size_t>((size_t)nthreads, (n + min_share - 1) / min_share);
+    if (t <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t step = ((n + t - 1) / t + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (int i = 1; i < t && (size_t)i * step < n; ++i) {
+        const size_t o = (size_t)i * step;
+        th.emplace_back(memcpy, dst + o, src + o, std::min(step, n - o));
+    }
+    memcpy(dst, src, std::min(step, n));
+    for (auto &x : th) x.join();
+}
+
 static bool pinned_host(const void *p)
 {
     if (!p) return false;
@@ -415,14 +444,19 @@ extern "C" int ss_score_batch_host(ss_ctx_t *c, const ss_batch_t *b, const ss_ou
     const struct { const void *src; size_t off, bytes; } in[5] = {
         {b->ref, o_ref, n}, {b->off_tumor, o_ot, 4 * (n + 1)}, {b->off_normal, o_on, 4 * (n + 1)},
         {b->reads_tumor, o_rt, 4 * nt}, {b->reads_normal, o_rn, 4 * nn}};
+    const int nthreads = copy_threads();
+    const size_t piece = (size_t)64 << 20;
     for (int k = 0; k < 5; ++k) {
         if (!in[k].bytes) continue;
-        const void *src = in[k].src;
-        if (!pinned_host(src)) {
-            memcpy(h + in[k].off, src, in[k].bytes);
-            src = h + in[k].off;
+        if (pinned_host(in[k].src)) {
+            HIPCHK(hipMemcpyAsync(d + in[k].off, in[k].src, in[k].bytes, hipMemcpyHostToDevice, s));
+            continue;
         }
-        HIPCHK(hipMemcpyAsync(d + in[k].off, src, in[k].bytes, hipMemcpyHostToDevice, s));
+        for (size_t p = 0; p < in[k].bytes; p += piece) {
+            const size_t nb = std::min(piece, in[k].bytes - p);
+            par_memcpy(h + in[k].off + p, (const char *)in[k].src + p, nb, nthreads);
+            HIPCHK(hipMemcpyAsync(d + in[k].off + p, h + in[k].off + p, nb, hipMemcpyHostToDevice, s));
+        }
     }
     ss_batch_t db = {n, (const uint8_t *)(d + o_ref), (const uint32_t *)(d + o_ot),
                      (const uint32_t *)(d + o_on), (const uint32_t *)(d + o_rt),
