@@ -248,15 +248,23 @@ int  ss_synth_batch_device(ss_ctx_t *ctx, const ss_synth_t *s, uint64_t first_si
                            uint32_t *reads_normal, uint64_t *n_reads_tumor,
                            uint64_t *n_reads_normal);
 
-/* HIP-event timing of the main scoring kernel, recorded on the stream each
+/* HIP-event timing of the scoring kernels, recorded on the stream each
  * ss_score_batch_device launch uses.  Enabling clears the log; every launch
- * while enabled appends one (start, stop) event pair (up to 4096).
+ * while enabled appends one set of events (up to 4096 launches).
  * ss_last_kernel_ms: duration of the latest launch (synchronizes on it), -1 if
  * none.  ss_kernel_time_log: durations of all logged launches in ms (waits for
  * them), returns how many were written to ms[0..cap). */
 int    ss_set_kernel_timing(ss_ctx_t *ctx, int enable);
 double ss_last_kernel_ms(ss_ctx_t *ctx);
 int    ss_kernel_time_log(ss_ctx_t *ctx, double *ms, int cap);
+/* The same log for one kernel of the launch sequence: SS_KT_MAIN
+ * (ss_score_main, as ss_kernel_time_log), SS_KT_WIDE (ss_score_wide),
+ * SS_KT_DEEP (ss_score_deep, LDS and giant), SS_KT_ALL (the whole launch). */
+#define SS_KT_MAIN 0
+#define SS_KT_WIDE 1
+#define SS_KT_DEEP 2
+#define SS_KT_ALL  3
+int    ss_kernel_time_log_k(ss_ctx_t *ctx, int kernel, double *ms, int cap);
 
 #ifdef __cplusplus
 }

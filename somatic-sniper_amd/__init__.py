@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "ss_abi_version", "ss_strerror", "ss_params_default", "ss_ctx_create", "ss_ctx_destroy",
     "ss_score_batch_device", "ss_score_batch_host", "ss_ctx_check", "ss_table_hashes",
     "ss_table_copy", "ss_synth_default", "ss_synth_batch_host", "ss_synth_batch_device",
-    "ss_set_kernel_timing", "ss_last_kernel_ms", "ss_kernel_time_log", "ss_model_check", "ss_model_pinned",
+    "ss_set_kernel_timing", "ss_last_kernel_ms", "ss_kernel_time_log", "ss_kernel_time_log_k", "ss_model_check", "ss_model_pinned",
     "ss_host_alloc", "ss_host_free",
 )
 
@@ -240,6 +240,7 @@ def load_library():
     lib.ss_model_check.argtypes = [vp, vp, vp]
     lib.ss_model_pinned.argtypes = [vp]
     lib.ss_kernel_time_log.argtypes = [vp, vp, C.c_int]
+    lib.ss_kernel_time_log_k.argtypes = [vp, C.c_int, vp, C.c_int]
     if lib.ss_abi_version() != 1:
         raise RuntimeError("libsniper_amd.so ABI mismatch")
     _LIB = lib
@@ -390,12 +391,15 @@ class Context:
     def last_kernel_ms(self) -> float:
         return float(self.lib.ss_last_kernel_ms(self.h))
 
-    def kernel_time_log(self) -> np.ndarray:
-        """Main-kernel durations (ms) of every launch since set_kernel_timing(True)."""
+    KERNELS = {"main": 0, "wide": 1, "deep": 2, "all": 3}   # SS_KT_*
+
+    def kernel_time_log(self, kernel: str = "main") -> np.ndarray:
+        """Durations (ms) of one kernel of every launch since set_kernel_timing(True):
+        "main" (ss_score_main), "wide", "deep" (LDS + giant) or "all" (the launch)."""
         buf = np.zeros(4096, np.float64)
-        n = self.lib.ss_kernel_time_log(self.h, buf.ctypes.data, buf.size)
+        n = self.lib.ss_kernel_time_log_k(self.h, self.KERNELS[kernel], buf.ctypes.data, buf.size)
         if n < 0:
-            raise SniperError(n, "ss_kernel_time_log")
+            raise SniperError(n, "ss_kernel_time_log_k")
         return buf[:n].copy()
 
     # -- reference-named single-site helpers ---------------------------------------

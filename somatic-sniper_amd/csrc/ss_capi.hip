@@ -22,6 +22,8 @@
 #include "ss_kernels.h"
 #include "ss_synth.h"
 
+#define SS_EV_PER_LAUNCH 4   /* before main, after main, after wide, after deep + giant */
+
 struct ss_ctx {
     int device;
     int n_cu;
@@ -37,7 +39,7 @@ struct ss_ctx {
     uint32_t giant_cap;
     uint32_t *d_giant_scratch;
     uint32_t giant_keys;
-    /* timing: a pool of event pairs, one pair per launch while enabled */
+    /* timing: a pool of events, SS_EV_PER_LAUNCH per launch while enabled */
     int timing;
     std::vector<hipEvent_t> *ev;
     int n_logged;
@@ -277,15 +279,14 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
                 (c->hm.prm.include_gor ? SS_MF_GOR : 0u);
     const int deep_grid = c->n_cu * 4;
     c->last_stream = s;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const hipEvent_t *evs = nullptr;
     if (c->timing && c->n_logged < 4096) {
-        while ((int)c->ev->size() < 2 * (c->n_logged + 1)) {
+        while ((int)c->ev->size() < SS_EV_PER_LAUNCH * (c->n_logged + 1)) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return SS_E_HIP;
             c->ev->push_back(e);
         }
-        e0 = (*c->ev)[2 * c->n_logged];
-        e1 = (*c->ev)[2 * c->n_logged + 1];
+        evs = c->ev->data() + SS_EV_PER_LAUNCH * c->n_logged;
         ++c->n_logged;
     }
     int wide_grid = c->n_cu;                      /* one 8-wave workgroup per CU fits (LDS) */
@@ -293,7 +294,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         const char *g = getenv("SS_WIDE_GRID");
         if (g && atoi(g) > 0 && atoi(g) <= 64) wide_grid = c->n_cu * atoi(g);
     }
-    int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, s, e0, e1);
+    int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, s, evs);
     return e == 0 ? SS_OK : SS_E_HIP;
 }
 
@@ -305,11 +306,14 @@ extern "C" int ss_set_kernel_timing(ss_ctx_t *c, int enable)
     return SS_OK;
 }
 
-static double pair_ms(ss_ctx_t *c, int i)
+/* launch i, kernel k: events k .. k+1 (k = 3: the whole launch, events 0 .. 3) */
+static double pair_ms(ss_ctx_t *c, int i, int k)
 {
     float ms = -1.0f;
-    if (hipEventSynchronize((*c->ev)[2 * i + 1]) != hipSuccess) return -1.0;
-    if (hipEventElapsedTime(&ms, (*c->ev)[2 * i], (*c->ev)[2 * i + 1]) != hipSuccess) return -1.0;
+    const hipEvent_t *ev = c->ev->data() + SS_EV_PER_LAUNCH * i;
+    const hipEvent_t a = k == SS_KT_ALL ? ev[0] : ev[k], b = k == SS_KT_ALL ? ev[3] : ev[k + 1];
+    if (hipEventSynchronize(b) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.0;
     return ms;
 }
 
@@ -317,17 +321,22 @@ extern "C" double ss_last_kernel_ms(ss_ctx_t *c)
 {
     if (!c || c->n_logged == 0) return -1.0;
     hipSetDevice(c->device);
-    return pair_ms(c, c->n_logged - 1);
+    return pair_ms(c, c->n_logged - 1, SS_KT_MAIN);
+}
+
+extern "C" int ss_kernel_time_log_k(ss_ctx_t *c, int kernel, double *ms, int cap)
+{
+    int i, n;
+    if (!c || (!ms && cap) || kernel < SS_KT_MAIN || kernel > SS_KT_ALL) return SS_E_INVAL;
+    hipSetDevice(c->device);
+    n = c->n_logged < cap ? c->n_logged : cap;
+    for (i = 0; i < n; ++i) ms[i] = pair_ms(c, i, kernel);
+    return n;
 }
 
 extern "C" int ss_kernel_time_log(ss_ctx_t *c, double *ms, int cap)
 {
-    int i, n;
-    if (!c || (!ms && cap)) return SS_E_INVAL;
-    hipSetDevice(c->device);
-    n = c->n_logged < cap ? c->n_logged : cap;
-    for (i = 0; i < n; ++i) ms[i] = pair_ms(c, i);
-    return n;
+    return ss_kernel_time_log_k(c, SS_KT_MAIN, ms, cap);
 }
 
 extern "C" int ss_ctx_check(ss_ctx_t *c)

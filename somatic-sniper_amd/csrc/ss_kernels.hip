@@ -1950,20 +1950,23 @@ __global__ void ss_synth_reads_kernel(ss_synth_k_t k, uint64_t first, uint64_t n
  * launchers
  * ------------------------------------------------------------------------ */
 int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, hipStream_t s,
-                    hipEvent_t ev0, hipEvent_t ev1)
+                    const hipEvent_t *ev)
 {
     hipError_t e;
-    if (ev0) (void)hipEventRecord(ev0, s);
+    if (ev) (void)hipEventRecord(ev[0], s);
     if (a.diag) hipLaunchKernelGGL(ss_score_main<true>, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     else hipLaunchKernelGGL(ss_score_main<false>, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    if (ev1) (void)hipEventRecord(ev1, s);
+    if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(ss_score_wide, dim3(wide_grid), dim3(SS_WIDE_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    if (ev) (void)hipEventRecord(ev[2], s);
     hipLaunchKernelGGL(ss_score_deep<false>, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(ss_score_deep<true>, dim3(SS_GIANT_BLOCKS), dim3(SS_DEEP_BLOCK), 0, s, a);
-    return (int)hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    if (ev) (void)hipEventRecord(ev[3], s);
+    return (int)hipSuccess;
 }
 
 int ss_launch_synth_depth(const ss_synth_k_t &k, uint64_t first, uint64_t n, uint8_t *ref,
