@@ -67,6 +67,9 @@
 #ifndef SS_PRIO_SORT
 #define SS_PRIO_SORT 3    /* wave priority raised over the sort network (A/B: +1.8%) */
 #endif
+#ifndef SS_WIDE_PREFETCH
+#define SS_WIDE_PREFETCH 1   /* wide kernel: next site's reads loaded into registers one site ahead */
+#endif
 #ifndef SS_PRIO_WIDE
 #define SS_PRIO_WIDE 1    /* the same over the wide kernel's network (A/B: +3.7% at 500x/500x) */
 #endif
@@ -1609,7 +1612,10 @@ void ss_score_main(ss_score_args a)
 namespace {
 
 #define WIDE_WAVES (SS_WIDE_BLOCK / 64)
-#define WIDE_ARENA (73728 / WIDE_WAVES)   /* u16 records per wave: 144 KB of LDS in all */
+#ifndef SS_WIDE_LDS_U16
+#define SS_WIDE_LDS_U16 73728              /* u16 fold records per workgroup: 144 KB of LDS */
+#endif
+#define WIDE_ARENA (SS_WIDE_LDS_U16 / WIDE_WAVES)   /* per wave */
 
 struct WideLds {
     uint16_t arena[WIDE_WAVES][WIDE_ARENA];
@@ -1742,7 +1748,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
         };
         if (nlist) {
             describe(0, s_cur, w_cur);
-            wide_load(a, w_cur, rd);
+            if (SS_WIDE_PREFETCH) wide_load(a, w_cur, rd);
         }
         while (i < nlist) {
             int G = 0;
@@ -1753,11 +1759,15 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
                 if (used + slots > WIDE_ARENA && !w.over) break;   /* next sub-group */
                 uint32_t cur[32];
+                if (SS_WIDE_PREFETCH) {
 #pragma unroll
-                for (int k = 0; k < 32; ++k) cur[k] = rd[k];
+                    for (int k = 0; k < 32; ++k) cur[k] = rd[k];
+                } else {
+                    wide_load(a, w, cur);
+                }
                 if (i + 1 < nlist) {
                     describe(i + 1, s_cur, w_cur);
-                    wide_load(a, w_cur, rd);
+                    if (SS_WIDE_PREFETCH) wide_load(a, w_cur, rd);
                 }
                 ++i;
                 if (w.over) {
