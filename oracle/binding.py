@@ -94,6 +94,15 @@ def load():
         lib.orc_glfgen.argtypes = [vp, vp, C.c_int, C.c_int, vp]
         lib.orc_glf2cns.argtypes = [vp, C.c_int]
         lib.orc_glf2cns.restype = C.c_uint32
+        # the reference's entry points under ss_ names (ss_oracle.c, end of file)
+        lib.ss_maqcns_init.argtypes = [vp]
+        lib.ss_maqcns_init.restype = vp
+        lib.ss_maqcns_destroy.argtypes = [vp]
+        lib.ss_maqcns_glfgen.argtypes = [vp, C.c_int, vp, C.c_int, vp]
+        lib.ss_glf2cns.argtypes = [vp, C.c_int]
+        lib.ss_glf2cns.restype = C.c_uint32
+        lib.ss_glf_somatic.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp, vp, vp]
+        lib.ss_glf_somatic.restype = C.c_int
         _LIB = lib
     return _LIB
 

@@ -466,3 +466,26 @@ long orc_score_batch(orc_model_t *m, uint64_t n_sites, const uint8_t *ref,
     }
     return ne;
 }
+
+/* ---- the reference's model API under ss_ names -----
+ * sniper_maqcns.h:23-29 and somatic_sniper.h:42 restated one-to-one so unit
+ * parity tests can call the reference's entry points by name:
+ *   ss_maqcns_init + ss_maqcns_prepare   sniper_maqcns_init/prepare (sniper_maqcns.c:102-118):
+ *                                         one call here, the params carry theta/n_hap/het_rate
+ *   ss_maqcns_destroy                    sniper_maqcns_destroy (:120-125)
+ *   ss_maqcns_glfgen                     sniper_maqcns_glfgen (:127-248); fills *g instead of
+ *                                         returning a calloc'd glf1_t
+ *   ss_glf2cns                           sniper_glf2cns (:250-273)
+ *   ss_glf_somatic                       glf_somatic (somatic_sniper.c:109-273) on packed reads */
+orc_model_t *ss_maqcns_init(const ss_params_t *p) { return orc_model_create(p); }
+void ss_maqcns_destroy(orc_model_t *m) { orc_model_destroy(m); }
+void ss_maqcns_glfgen(orc_model_t *m, int n, const uint32_t *reads, int ref_nt16, ss_glf_t *g)
+{
+    orc_glfgen(m, reads, n, ref_nt16, g);
+}
+uint32_t ss_glf2cns(const ss_glf_t *g, int q_r) { return orc_glf2cns(g, q_r); }
+int ss_glf_somatic(orc_model_t *m, int ref_char, int n1, const uint32_t *pl1, int n2, const uint32_t *pl2,
+                   ss_glf_t *g1, ss_glf_t *g2, ss_call_t *call)
+{
+    return orc_site(m, ref_char, pl1, n1, pl2, n2, g1, g2, call);
+}

@@ -78,3 +78,43 @@ def test_oracle_matches_reference_golden(oracle, same_tables_as_build_host, path
                 assert int(f[5]) == c["somatic_score"]
                 assert int(f[6]) == (c["cns_tumor"] >> 8) & 0xFF
                 assert int(f[7]) == c["snp_q_tumor"] and int(f[10]) == c["snp_q_normal"]
+
+
+def test_reference_named_entry_points(oracle, same_tables_as_build_host):
+    """The model API under the reference's names (SURVEY.md section 8b:
+    ss_maqcns_init / ss_maqcns_glfgen / ss_glf2cns / ss_glf_somatic /
+    ss_maqcns_destroy), called site by site as sniper_pileup.c:256-258 calls
+    glf_somatic, against the reference's golden returns, glf records and
+    consensus words."""
+    import ctypes as C
+    z = np.load(os.path.join(HERE, "golden", "c60x.npz"), allow_pickle=False)
+    lib = oracle.load()
+    o = oracle.Oracle()                                  # default params, as z's "default" set
+    m = lib.ss_maqcns_init(C.byref(o.params))
+    assert m
+    try:
+        q_r = int(lib.orc_model_q_r(m) + 0.5)
+        ot, on = z["off_tumor"], z["off_normal"]
+        rt = np.ascontiguousarray(z["reads_tumor"], np.uint32)
+        rn = np.ascontiguousarray(z["reads_normal"], np.uint32)
+        call = (C.c_uint8 * 64)()
+        n = min(400, z["ref"].shape[0])
+        glf_ref = z["glf_default"]                       # (n, 2 x 20 B ss_glf_t)
+        gsz = glf_ref.shape[1] // 2
+        for i in range(n):
+            g2 = (C.c_uint8 * 64)()
+            nt, nn = int(ot[i + 1] - ot[i]), int(on[i + 1] - on[i])
+            pt = rt[ot[i]:].ctypes.data if nt else None
+            pn = rn[on[i]:].ctypes.data if nn else None
+            r = lib.ss_glf_somatic(m, int(z["ref"][i]), nt, pt, nn, pn, g2, C.byref(g2, gsz), call)
+            assert r == int(z["ret_default"][i]), i
+            assert bytes(g2)[:2 * gsz] == glf_ref[i].tobytes(), i
+            if r >= 0:
+                cns = [lib.ss_glf2cns(C.byref(g2, k * gsz), q_r) for k in (0, 1)]
+                assert cns == z["cns_default"][i].tolist(), i
+            # glfgen alone (tumor) equals glf_somatic's tumor record
+            g1 = (C.c_uint8 * 64)()
+            lib.ss_maqcns_glfgen(m, nt, pt, int(lib.orc_nt16_of(int(z["ref"][i]))), g1)
+            assert bytes(g1)[:gsz] == bytes(g2)[:gsz], i
+    finally:
+        lib.ss_maqcns_destroy(m)
