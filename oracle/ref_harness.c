@@ -239,7 +239,7 @@ static double now_s(void)
 static int cmd_synth(int argc, char **argv, opts_t *o)
 {
     ss_synth_t s;
-    uint64_t ns, done = 0, seed = 0x5EED5A1DC0FFEE01ull, h = FNV0, reads = 0;
+    uint64_t ns, done = 0, first = 0, seed = 0x5EED5A1DC0FFEE01ull, h = FNV0, reads = 0;
     uint32_t shard = 0;
     const char *scores_fn = NULL;
     FILE *sf = NULL, *txt;
@@ -257,6 +257,7 @@ static int cmd_synth(int argc, char **argv, opts_t *o)
     for (a = 5; a < argc; ++a) {
         if (!strcmp(argv[a], "--seed")) seed = strtoull(argv[++a], NULL, 0);
         else if (!strcmp(argv[a], "--shard")) shard = (uint32_t)atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--first")) first = strtoull(argv[++a], NULL, 0);   /* sites [first, first + n) */
         else if (!strcmp(argv[a], "--scores")) scores_fn = argv[++a];
         else if (!parse_opt(o, argc, argv, &a)) { fprintf(stderr, "bad opt %s\n", argv[a]); return 2; }
     }
@@ -273,10 +274,10 @@ static int cmd_synth(int argc, char **argv, opts_t *o)
     while (done < ns) {
         uint64_t m = ns - done < (uint64_t)chunk ? ns - done : (uint64_t)chunk, i, nt, nn;
         double t0;
-        ss_synth_batch_host(&s, done, m, ref, ot, on, NULL, NULL, &nt, &nn);
+        ss_synth_batch_host(&s, first + done, m, ref, ot, on, NULL, NULL, &nt, &nn);
         if (nt > rtc) { rtc = nt; rt = (uint32_t *)realloc(rt, 4 * rtc); }
         if (nn > rnc) { rnc = nn; rn = (uint32_t *)realloc(rn, 4 * rnc); }
-        ss_synth_batch_host(&s, done, m, ref, ot, on, rt, rn, &nt, &nn);
+        ss_synth_batch_host(&s, first + done, m, ref, ot, on, rt, rn, &nt, &nn);
         reads += nt + nn;
         if (!d) d = setup(o, (const char *)ref, chunk, txt, &fmt);
         d->ref = (char *)ref; d->len = (int)m;
@@ -315,6 +316,6 @@ int main(int argc, char **argv)
     if (!strcmp(argv[1], "dump")) { int r = cmd_dump(argc, argv, &o); if (r == 2) goto usage; return r; }
     if (!strcmp(argv[1], "synth")) { int r = cmd_synth(argc, argv, &o); if (r == 2) goto usage; return r; }
 usage:
-    fprintf(stderr, "usage: ref_harness tables | dump BATCH OUT TXT [opts] | synth LT LN N [--seed S] [--shard K] [--scores F] [opts]\n");
+    fprintf(stderr, "usage: ref_harness tables | dump BATCH OUT TXT [opts] | synth LT LN N [--seed S] [--shard K] [--first I] [--scores F] [opts]\n");
     return 2;
 }

@@ -254,6 +254,40 @@ def test_gpu_matches_real_reference_on_this_host(pkg, tmp_path):
         assert len(calls) == txt.count("\n")
 
 
+def test_full_size_batch_vs_real_reference(pkg, ctx, tmp_path):
+    """2^22 sites of the BASELINE workload (60x/30x, default seed, shard 0),
+    generated and scored in HBM, against the compiled reference's glf_somatic
+    on the same sites run on this host by 16 processes (oracle/_ref/ref_harness
+    synth --first): every site's return value bit-exact."""
+    import os
+    import subprocess
+    torch = pytest.importorskip("torch")
+    from oracle import binding as ob
+    if not os.path.exists(ob.REF_HARNESS):
+        pytest.skip("reference harness not built")
+    n, procs = 1 << 22, 16
+    d = ctx.synth_device(pkg.Synth.default(60, 30), 0, n)
+    score = torch.empty(n, dtype=torch.int32, device=d["ref"].device)
+    ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                     score=score)
+    ctx.check()
+    gpu = score.cpu().numpy()
+    step = n // procs
+    runs = []
+    for k in range(procs):
+        out = str(tmp_path / f"s{k}.bin")
+        runs.append((out, subprocess.Popen([ob.REF_HARNESS, "synth", "60", "30", str(step), "--first",
+                                            str(k * step), "--scores", out],
+                                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)))
+    for out, p in runs:
+        assert p.wait(timeout=100) == 0, p.stderr.read()[-500:]
+    ref = np.concatenate([np.fromfile(out, np.int32) for out, _ in runs])
+    assert ref.shape == (n,)
+    bad = np.nonzero(gpu != ref)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first {bad[:5]}: gpu {gpu[bad[:5]]} reference {ref[bad[:5]]}"
+    assert (ref == 255).sum() > n // 2 and (ref > 0).sum() > 0
+
+
 def test_tables_equal_reference_on_this_host(pkg):
     import json
     import os
