@@ -254,19 +254,22 @@ def test_gpu_matches_real_reference_on_this_host(pkg, tmp_path):
         assert len(calls) == txt.count("\n")
 
 
-def test_full_size_batch_vs_real_reference(pkg, ctx, tmp_path):
-    """2^22 sites of the BASELINE workload (60x/30x, default seed, shard 0),
-    generated and scored in HBM, against the compiled reference's glf_somatic
-    on the same sites run on this host by 16 processes (oracle/_ref/ref_harness
-    synth --first): every site's return value bit-exact."""
+@pytest.mark.parametrize("lt,ln,n", [(60, 30, 1 << 22), (30, 30, 1 << 22), (100, 60, 1 << 21),
+                                     (500, 500, 1 << 16)])
+def test_full_size_batch_vs_real_reference(pkg, ctx, tmp_path, lt, ln, n):
+    """Large batches of the BASELINE depth configurations (C4 60x/30x -- the
+    headline --, C2, C3, C5; default seed, shard 0), generated and scored in
+    HBM, against the compiled reference's glf_somatic on the same sites run on
+    this host by 16 processes (oracle/_ref/ref_harness synth --first): every
+    site's return value bit-exact."""
     import os
     import subprocess
     torch = pytest.importorskip("torch")
     from oracle import binding as ob
     if not os.path.exists(ob.REF_HARNESS):
         pytest.skip("reference harness not built")
-    n, procs = 1 << 22, 16
-    d = ctx.synth_device(pkg.Synth.default(60, 30), 0, n)
+    procs = 16
+    d = ctx.synth_device(pkg.Synth.default(lt, ln), 0, n)
     score = torch.empty(n, dtype=torch.int32, device=d["ref"].device)
     ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
                      score=score)
@@ -276,7 +279,7 @@ def test_full_size_batch_vs_real_reference(pkg, ctx, tmp_path):
     runs = []
     for k in range(procs):
         out = str(tmp_path / f"s{k}.bin")
-        runs.append((out, subprocess.Popen([ob.REF_HARNESS, "synth", "60", "30", str(step), "--first",
+        runs.append((out, subprocess.Popen([ob.REF_HARNESS, "synth", str(lt), str(ln), str(step), "--first",
                                             str(k * step), "--scores", out],
                                            stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)))
     for out, p in runs:
@@ -285,7 +288,7 @@ def test_full_size_batch_vs_real_reference(pkg, ctx, tmp_path):
     assert ref.shape == (n,)
     bad = np.nonzero(gpu != ref)[0]
     assert bad.size == 0, f"{bad.size} mismatches, first {bad[:5]}: gpu {gpu[bad[:5]]} reference {ref[bad[:5]]}"
-    assert (ref == 255).sum() > n // 2 and (ref > 0).sum() > 0
+    assert (ref == 255).sum() > n // 2
 
 
 def test_tables_equal_reference_on_this_host(pkg):
