@@ -814,7 +814,6 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
 }
 
 
-__device__ __forceinline__ uint32_t halfswap(uint32_t x) { return (x >> 16) | (x << 16); }
 
 /* Bitonic sort (the "flip" formulation: every comparator puts the minimum at
  * the lower index, so all directions are single lane bits), ascending, of
