@@ -67,6 +67,9 @@
 #ifndef SS_PRIO_SORT
 #define SS_PRIO_SORT 3    /* wave priority raised over the sort network (A/B: +1.8%) */
 #endif
+#ifndef SS_GENO_BATCH
+#define SS_GENO_BATCH 3   /* likelihood gathers issued together, this many genotypes at a time (geno_p5; 0: one by one; 5 spills 12 B) */
+#endif
 #ifndef SS_WIDE_PREFETCH
 #define SS_WIDE_PREFETCH 1   /* wide kernel: next site's reads loaded into registers one site ahead */
 #endif
@@ -299,6 +302,69 @@ __device__ __forceinline__ float geno_p(int j, int k, const float es[4], const f
         v = hom ? 0.0f : (float)lh;
     }
     return v < 0.0f ? 0.0f : v;
+}
+
+/* geno_p for the five genotypes role * 5 + t of one lane, with every table
+ * gather issued before any is consumed: indices are computed unconditionally
+ * (an unused one points at entry 0), so the ten loads go out back to back and
+ * the lane waits for memory once instead of once per genotype and table.  The
+ * arithmetic on the loaded values is geno_p's, operation for operation. */
+template <int T0, int T1>
+__device__ __forceinline__ void geno_p_range(uint32_t role, const float es[4], const float fs[4],
+                                             const uint32_t c[4], uint32_t tot, const ss_dev_model &m,
+                                             float out[5])
+{
+    float ev[5];
+    uint32_t c2v[5];
+    bool homv[5];
+    double lhv[5], cfv[5];
+#pragma unroll
+    for (int t = T0; t < T1; ++t) {
+        int j, k;
+        geno_jk((int)role * 5 + t, j, k);
+        float e = 0.0f, f = 0.0f;
+        uint32_t c2 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool use = i != j && i != k;
+            e = use ? e + es[i] : e;
+            f = use ? f + fs[i] : f;
+            c2 += use ? c[i] : 0u;
+        }
+        const bool hom = j == k;
+        const uint32_t il = hom ? 0u : (c[j] << 8 | c[k]);
+        const uint32_t ic = c2 ? ((uint32_t)clamp_bar_e(e, f) << 16 | tot << 8 | c2) : 0u;
+        lhv[t] = ss_tab_lhet(m)[il];
+        cfv[t] = ss_tab_coef(m)[ic];
+        ev[t] = e;
+        c2v[t] = c2;
+        homv[t] = hom;
+    }
+#pragma unroll
+    for (int t = T0; t < T1; ++t) {
+        const double lh = homv[t] ? 0.0 : -4.343 * lhv[t];
+        float v;
+        if (c2v[t]) v = homv[t] ? (float)((double)ev[t] + cfv[t]) : (float)((lh + (double)ev[t]) + cfv[t]);
+        else v = homv[t] ? 0.0f : (float)lh;
+        out[t] = v < 0.0f ? 0.0f : v;
+    }
+}
+
+/* the five genotypes in batches of SS_GENO_BATCH (register pressure) */
+__device__ __forceinline__ void geno_p5(uint32_t role, const float es[4], const float fs[4],
+                                        const uint32_t c[4], uint32_t tot, const ss_dev_model &m,
+                                        float out[5])
+{
+    if constexpr (SS_GENO_BATCH >= 5) {
+        geno_p_range<0, 5>(role, es, fs, c, tot, m, out);
+    } else if constexpr (SS_GENO_BATCH >= 3) {
+        geno_p_range<0, 3>(role, es, fs, c, tot, m, out);
+        geno_p_range<3, 5>(role, es, fs, c, tot, m, out);
+    } else {
+        geno_p_range<0, 2>(role, es, fs, c, tot, m, out);
+        geno_p_range<2, 4>(role, es, fs, c, tot, m, out);
+        geno_p_range<4, 5>(role, es, fs, c, tot, m, out);
+    }
 }
 
 /* counts rescale of sniper_maqcns.c:178-182 */
@@ -1418,11 +1484,17 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     uint32_t c[4];
     const uint32_t tot = rescale_counts(cnt, c);
     float mine[5];
+    if (SS_GENO_BATCH > 0) {
+        geno_p5(role, es, fs, c, tot, a.m, mine);
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-        int j, k;
-        geno_jk((int)role * 5 + t, j, k);
-        mine[t] = (act && !(diag & 4u)) ? geno_p(j, k, es, fs, c, tot, a.m) : 0.0f;
+        for (int t = 0; t < 5; ++t) mine[t] = (act && !(diag & 4u)) ? mine[t] : 0.0f;
+    } else {
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            int j, k;
+            geno_jk((int)role * 5 + t, j, k);
+            mine[t] = (act && !(diag & 4u)) ? geno_p(j, k, es, fs, c, tot, a.m) : 0.0f;
+        }
     }
     float p[10];
 #pragma unroll
