@@ -1702,6 +1702,7 @@ struct WideLds {
  * ahead of its sort so the HBM latency overlaps the previous site's work. */
 struct WideSite {
     uint32_t ot, nt, on, nn;
+    uint32_t ref;      /* ref char | nt16 code << 8, loaded with the offsets (one site ahead) */
     bool split;        /* split placement (see split_fits): top level skipped */
     bool over;         /* more than SS_WIDE_MAXSLOTS slots (or a wrapped count): deep kernel */
 };
@@ -1807,7 +1808,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
         const uint32_t nlist = scount - first < GB ? scount - first : GB;
         /* site i's reads are in flight while site i-1 is sorted */
         uint32_t i = 0, s_cur = 0;
-        WideSite w_cur = {0, 0, 0, 0, false, false};
+        WideSite w_cur = {0, 0, 0, 0, 0, false, false};
         uint32_t rd[32];
         auto describe = [&](uint32_t k, uint32_t &s, WideSite &w) {
             s = list[first + k];
@@ -1815,6 +1816,8 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
             w.nt = a.off_t[s + 1] - w.ot;
             w.on = a.off_n[s];
             w.nn = a.off_n[s + 1] - w.on;
+            const uint32_t rc = a.ref[s];
+            w.ref = rc | (uint32_t)ss_tab_nt16(a.m)[rc] << 8;
             wide_place(w);
         };
         if (nlist) {
@@ -1849,8 +1852,8 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                     }
                     continue;
                 }
-                const uint32_t refc = a.ref[s];
-                const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
+                const uint32_t refc = w.ref & 0xffu;
+                const uint32_t ref16 = w.ref >> 8;
                 if (slots <= 1024u)
                     sort_site_wide<8>(cur, w, ref16, cap, arena, used, slot + 2 * G);
                 else
