@@ -486,8 +486,8 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
                             const SlotRes &rt, const SlotRes &rn)
 {
     const ss_dev_model &m = a.m;
-    const int rb = (int)refc;
-    const int rb4 = ss_tab_nt16(m)[refc & 0xffu];
+    const int rb = (int)(refc & 0xffu);      /* refc: ref char | nt16 code << 8 */
+    const int rb4 = (int)(refc >> 8);
     if (!(rb != 'N' && rt.depth > 0u && rn.depth > 0u)) { a.score[site] = -1; return; }
     const uint32_t ct = rt.cns, cn = rn.cns;
     const int t1 = (int)(ct >> 28), t2 = (int)(ct >> 24 & 0xf), ts1 = (int)(ct >> 8 & 0xff), ts2 = (int)(ct & 0xff);
@@ -638,7 +638,7 @@ __device__ __forceinline__ void finish_group(const ss_score_args &a, int G, cons
             r.rms_q = (uint8_t)rms_q;
             if (a.glf) {
                 const uint32_t site = sinfo[s].site;
-                const uint32_t ref16 = ss_tab_nt16(a.m)[sinfo[s].refc & 0xffu];
+                const uint32_t ref16 = sinfo[s].refc >> 8;
                 store_glf(&a.glf[2ull * site + (slot & 1)], ref16, lk, min_lk, rms_q, r.depth);
             }
         }
@@ -1521,7 +1521,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         r.depth = depth;
         if (a.glf) {
             const uint32_t s = (uint32_t)sl >> 1;
-            store_glf(&a.glf[2ull * sites[s] + (sl & 1)], ss_tab_nt16(a.m)[refcs[s] & 0xffu], lk, min_lk,
+            store_glf(&a.glf[2ull * sites[s] + (sl & 1)], refcs[s] >> 8, lk, min_lk,
                       rms_q, depth);
         }
     }
@@ -1619,7 +1619,7 @@ void ss_score_main(ss_score_args a)
                 tot[m] = S2[m].nt + (S2[m].nt & 1u) + S2[m].nn;   /* sort slots incl. pad */
                 if (lane == 0 && i + (uint32_t)m < cur.b) {
                     sites[G + m] = (uint32_t)(blk * GB + j);
-                    refcs[G + m] = rdesc & 0xffu;
+                    refcs[G + m] = rdesc & 0xffffu;      /* ref char | nt16 << 8 */
                 }
             }
             if (i + 1u < cur.b && tot[0] <= 256u && tot[1] <= 256u) {   /* two sites, interleaved */
@@ -1852,7 +1852,6 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                     }
                     continue;
                 }
-                const uint32_t refc = w.ref & 0xffu;
                 const uint32_t ref16 = w.ref >> 8;
                 if (slots <= 1024u)
                     sort_site_wide<8>(cur, w, ref16, cap, arena, used, slot + 2 * G);
@@ -1860,7 +1859,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                     sort_site_wide<16>(cur, w, ref16, cap, arena, used, slot + 2 * G);
                 if (lane == 0) {
                     sites[G] = s;
-                    refcs[G] = refc;
+                    refcs[G] = w.ref;
                 }
                 used += slots;
                 ++G;
@@ -1983,7 +1982,7 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
         }
         const uint32_t refc = a.ref[s];
         const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
-        if (threadIdx.x == 0) { D.sinfo[0].site = s; D.sinfo[0].refc = refc; }
+        if (threadIdx.x == 0) { D.sinfo[0].site = s; D.sinfo[0].refc = refc | ref16 << 8; }
         deep_sample(a.reads_t + ot, nt, ref16, cap, bt, D, 0);
         deep_sample(a.reads_n + on, nn, ref16, cap, bn, D, 1);
         __syncthreads();
