@@ -9,7 +9,11 @@ timing; the timed region contains only scoring.
 Multi-GPU: one process per GPU (torch.distributed, RCCL backend only for the
 barrier and the max-over-ranks timing reduction).  Each rank scores its own
 genome shard (synth shard = rank) -- no collective on the data path, weak
-scaling.  value = sites scored by all ranks / max rank time.
+scaling.  value = sites scored by all ranks / max rank time.  Launched either
+by torch.distributed.run (RANK/WORLD_SIZE/LOCAL_RANK in the environment) or
+directly as ``bench.py --gpus N``: the parent then starts N fresh rank
+processes itself before anything touches the GPU, stays GPU-free, and relays
+rank 0's line.
 
 Extra fields: "roofline" (main kernel, HIP events over the timed region,
 algorithmic bytes 4 B/read + 16 B/site), "cpu_baseline" (the real reference
@@ -67,7 +71,7 @@ def cpu_baseline(lt, ln, sample, seed, gpu_scores_prefix):
     parity = None
     if gpu_scores_prefix is not None and len(gpu_scores_prefix) >= sample:
         parity = bool((gpu_scores_prefix[:sample] == cpu_scores).all())
-    return {"value": round(value, 1), "unit": "sites/s", "cores": 1, "kind": kind,
+    return {"value": round(value, 1), "unit": "sites/s", "cores": 1, "kind": kind, "cpu_model": cpu_model(),
             "sample": desc, "parity_vs_gpu": parity}
 
 
@@ -79,7 +83,7 @@ def cpu_baseline_all_cores(lt, ln, seed, per_proc=500_000):
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.path.exists(harness):
         return None
-    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    cores, cores_source = host_cores()
     procs = [subprocess.Popen([harness, "synth", str(lt), str(ln), str(per_proc), "--seed", str(seed),
                                "--shard", str(100 + k)], stdout=subprocess.PIPE, text=True)
              for k in range(cores)]
@@ -90,9 +94,81 @@ def cpu_baseline_all_cores(lt, ln, seed, per_proc=500_000):
             return None
         secs.append(json.loads(out.strip().splitlines()[-1])["seconds"])
     return {"value": round(cores * per_proc / max(secs), 1), "unit": "sites/s", "cores": cores,
-            "kind": "reference",
+            "kind": "reference", "cpu_model": cpu_model(), "cores_source": cores_source,
+            "host_cpus": os.cpu_count(),
             "sample": f"{cores} concurrent processes x {per_proc} synthetic sites ({lt}xT/{ln}xN, own shard each), "
                       f"reference glf_somatic only, total sites / longest process time"}
+
+
+# library tuning / diagnostic switches that must not leak into a timed run
+REFUSED_ENV = ("SS_DIAG", "SS_MAIN_GRID", "SS_WIDE_GRID", "SNIPER_AMD_LIB")
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv=None, script=None) -> int:
+    """Start n rank processes of this script (RANK/WORLD_SIZE/LOCAL_RANK set), one
+    per GPU, and wait for them.  Called before the parent imports torch or touches
+    a device: every rank is a fresh process that initialises only its own GPU.
+    If one rank fails the others are stopped (by PID) and its exit code returned."""
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)]
+                                      + list(sys.argv[1:] if argv is None else argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.terminate()
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def host_cores():
+    """CPUs this process may use: the cgroup CPU quota when one is set (a GPU box
+    grants a share of a larger host), else the affinity mask (nproc)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, -(-int(quota) // int(period))), "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    try:
+        return len(os.sched_getaffinity(0)), "sched_getaffinity (nproc)"
+    except AttributeError:
+        return os.cpu_count() or 1, "os.cpu_count"
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
@@ -100,7 +176,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--sites", type=int, default=1 << 24, help="sites per batch (per step, per GPU)")
+    ap.add_argument("--sites", type=int, default=1 << 26, help="sites per batch (per step, per GPU)")
     ap.add_argument("--batches", type=int, default=2, help="distinct resident batches cycled per rank")
     ap.add_argument("--lt", type=float, default=60.0)
     ap.add_argument("--ln", type=float, default=30.0)
@@ -112,14 +188,28 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
+    bad = [k for k in REFUSED_ENV if os.environ.get(k)]
+    if bad:
+        sys.exit(f"bench.py: refusing to time with tuning/diagnostic variables set: {', '.join(bad)}")
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(spawn_ranks(args.gpus))      # parent: no torch, no GPU
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
     if args.backend != "nccl":
-        local %= max(1, torch.cuda.device_count())   # rehearsal: ranks share the visible GPUs
+        local %= max(1, ndev)                       # rehearsal: ranks share the visible GPUs
+    elif local >= ndev:
+        sys.exit(f"bench.py: rank {rank} needs cuda:{local} but {ndev} device(s) are visible")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -133,6 +223,7 @@ def main():
     from __graft_entry__ import load_package
     pkg = load_package()
     ctx = pkg.Context(pkg.Params.default(), device=local)
+    pinned = pkg.model_check()["pinned"]
 
     # ---- resident synthetic batches (this rank's shard) ----
     S = args.sites
@@ -142,6 +233,8 @@ def main():
         d = ctx.synth_device(syn, b * S, S, device=dev)
         batches.append(d)
     torch.cuda.synchronize(dev)
+    if max(max(d["n_reads"]) for d in batches) >= 1 << 32:
+        sys.exit("bench.py: a batch holds >= 2^32 reads of one sample (u32 offsets); lower --sites")
     reads = [sum(d["n_reads"]) for d in batches]
     bytes_per_batch = [4 * r + 16 * S for r in reads]
     score = [torch.empty(S, dtype=torch.int32, device=dev) for _ in batches]
@@ -187,7 +280,18 @@ def main():
     sites_rank = S * args.steps
     import importlib
     sharding = importlib.import_module("somatic_sniper_amd.sharding")
+    rank_elapsed = elapsed
     elapsed, total_sites, _ = sharding.aggregate(elapsed, sites_rank, world)
+    prop = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "device": local, "pci_bus_id": getattr(prop, "pci_bus_id", None),
+          "ms_per_step": round(rank_elapsed / args.steps * 1e3, 4), "sites": sites_rank}
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    else:
+        ranks = [me]
+    if rank == 0:
+        print(f"bench: ranks {[(r['rank'], r['device'], r['pci_bus_id']) for r in ranks]}", file=sys.stderr)
 
     avg_kernel_ms = float(np.mean(kms)) if len(kms) else None
     alg_bytes = float(np.mean([bytes_per_batch[k] for k in used]))
@@ -217,7 +321,9 @@ def main():
         "config": {"workload": f"synthetic WGS shard per GPU, {args.lt:g}xT/{args.ln:g}xN Poisson depth",
                    "sites_per_step_per_gpu": S, "resident_batches": len(batches),
                    "mean_reads_per_site": round(float(np.mean(reads)) / S, 2),
-                   "parallelism": f"region-sharded x{world}, no collectives"},
+                   "parallelism": f"region-sharded x{world}, no collectives",
+                   "model_tables_pinned": pinned},
+        "ranks": ranks,
         "roofline": {
             "bound": "hbm",
             "kernel": {"main": "ss_score_main", "wide": "ss_score_wide", "deep": "ss_score_deep"}[dom],
