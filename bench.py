@@ -100,8 +100,18 @@ def cpu_baseline_all_cores(lt, ln, seed, per_proc=500_000):
                       f"reference glf_somatic only, total sites / longest process time"}
 
 
-# library tuning / diagnostic switches that must not leak into a timed run
-REFUSED_ENV = ("SS_DIAG", "SS_MAIN_GRID", "SS_WIDE_GRID", "SNIPER_AMD_LIB")
+# tuning / diagnostic switches of earlier builds: refused so that no timed run
+# can be mistaken for one made with them (the shipped library reads none)
+REFUSED_ENV = ("SS_DIAG", "SS_MAIN_GRID", "SS_WIDE_GRID")
+
+
+def library_id(pkg):
+    """Path (relative to the repo) and content hash of the scoring library used."""
+    import hashlib
+    path = pkg.library_path()
+    with open(path, "rb") as f:
+        digest = hashlib.sha256(f.read()).hexdigest()[:16]
+    return {"path": os.path.relpath(path, ROOT), "sha256_16": digest}
 
 
 def free_port() -> int:
@@ -322,7 +332,7 @@ def main():
                    "sites_per_step_per_gpu": S, "resident_batches": len(batches),
                    "mean_reads_per_site": round(float(np.mean(reads)) / S, 2),
                    "parallelism": f"region-sharded x{world}, no collectives",
-                   "model_tables_pinned": pinned},
+                   "model_tables_pinned": pinned, "library": library_id(pkg)},
         "ranks": ranks,
         "roofline": {
             "bound": "hbm",

@@ -164,15 +164,19 @@ int  ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out);
 void ss_ctx_destroy(ss_ctx_t *ctx);
 
 /* Score a device-resident batch, asynchronously on `stream` (a hipStream_t,
- * NULL = default stream).  All batch/out pointers are device pointers. */
+ * NULL = default stream).  All batch/out pointers are device pointers.
+ * Launches of one context share its work lists, so they run one after the
+ * other: a launch on another stream than the previous one (or the host path's
+ * own stream) first waits for the previous launch on the device.  Use one
+ * context per stream for concurrent batches.  No depth limit: sites of any
+ * depth are scored. */
 int  ss_score_batch_device(ss_ctx_t *ctx, const ss_batch_t *batch,
                            const ss_out_t *out, void *stream);
 
 /* Wait for the context's outstanding work and report sticky device-side
- * errors: SS_E_INVAL if a batch had decreasing read offsets, else
- * SS_E_CAPACITY if a work list overflowed or a site exceeded the giant scratch
- * (such sites carry score -2; so does a site whose offsets decrease -- the
- * kernels never read reads for it).  Clears the sticky bits. */
+ * errors: SS_E_INVAL if a batch had malformed read offsets (a site whose
+ * offsets decrease or pass off[n_sites]: it scores -2 and no read is loaded
+ * for it).  Clears the sticky bits. */
 int  ss_ctx_check(ss_ctx_t *ctx);
 
 /* Score a host batch: stages through pinned buffers, H2D, kernel, D2H, sorts
@@ -259,7 +263,7 @@ double ss_last_kernel_ms(ss_ctx_t *ctx);
 int    ss_kernel_time_log(ss_ctx_t *ctx, double *ms, int cap);
 /* The same log for one kernel of the launch sequence: SS_KT_MAIN
  * (ss_score_main, as ss_kernel_time_log), SS_KT_WIDE (ss_score_wide),
- * SS_KT_DEEP (ss_score_deep, LDS and giant), SS_KT_ALL (the whole launch). */
+ * SS_KT_DEEP (ss_score_deep), SS_KT_ALL (the whole launch). */
 #define SS_KT_MAIN 0
 #define SS_KT_WIDE 1
 #define SS_KT_DEEP 2

@@ -162,7 +162,10 @@ static void shim_flush(void)
     for (;;) {
         ss_out_t o = {g_b.score, g_b.calls, (uint32_t)g_b.calls_cap, &ncalls, NULL, &nclamp};
         int rc = ss_score_batch_host(g_ctx, &b, &o);
-        if (rc == SS_E_CAPACITY) {
+        /* grow and re-score only when the emitted calls did not fit; any
+         * other error (including a capacity error of the device work lists)
+         * is final */
+        if (rc == SS_E_CAPACITY && ncalls > g_b.calls_cap) {
             size_t c = g_b.calls_cap;
             g_b.calls = grow(g_b.calls, &c, ncalls, sizeof(ss_call_t));
             g_b.calls_cap = c;

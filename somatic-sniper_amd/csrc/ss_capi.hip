@@ -5,7 +5,7 @@
  * Memory layout in HBM per context (DESIGN.md "Data layout"):
  *   model   coef 32 MiB + lhet 512 KiB + fk 2 KiB + qadd/prior/jprior/nt16 12 KiB
  *           (read-only, stays resident in L2/MALL after the first batches)
- *   lists   deep/giant site lists + counters, giant scratch 64 MiB
+ *   lists   deep site lists + counters (sized from the batch)
  *   host-path staging buffers, grown on demand
  */
 #include <hip/hip_runtime.h>
@@ -31,19 +31,17 @@ struct ss_ctx {
     /* model on the device */
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
-    uint32_t *d_counters;     /* [0] unused, [1] giant, [2] err, [3] scratch n_calls, [4] clamped, [5] deep2 */
+    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
-    uint32_t *d_deep_seg;     /* per-main-wave deep segment lengths [n_cu * 16 * 4] */
-    uint32_t *d_giant_list;
-    uint32_t giant_cap;
-    uint32_t *d_giant_scratch;
-    uint32_t giant_keys;
+    uint32_t *d_deep_seg;     /* per-main-wave deep segment lengths */
     /* timing: a pool of events, SS_EV_PER_LAUNCH per launch while enabled */
     int timing;
     std::vector<hipEvent_t> *ev;
     int n_logged;
     hipStream_t last_stream;
+    hipEvent_t done;          /* recorded after every launch: the next launch on another stream waits */
+    int launched;
     /* host path */
     hipStream_t hstream;
     void *h_stage;  size_t h_stage_sz;     /* pinned */
@@ -95,8 +93,8 @@ extern "C" void ss_ctx_destroy(ss_ctx_t *c)
     if (!c) return;
     hipSetDevice(c->device);
     hipDeviceSynchronize();
-    void *ptrs[] = {c->d_tab, c->d_counters, c->d_deep_list, c->d_deep_seg, c->d_giant_list, c->d_giant_scratch, c->d_stage,
-                    c->d_cdf, c->d_scan_tmp, c->d_depth_tmp};
+    void *ptrs[] = {c->d_tab, c->d_counters, c->d_deep_list, c->d_deep_seg, c->d_stage, c->d_cdf, c->d_scan_tmp,
+                    c->d_depth_tmp};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (c->h_stage) hipHostFree(c->h_stage);
@@ -105,6 +103,7 @@ extern "C" void ss_ctx_destroy(ss_ctx_t *c)
         delete c->ev;
     }
     if (c->hstream) hipStreamDestroy(c->hstream);
+    if (c->done) hipEventDestroy(c->done);
     ss_host_model_free(&c->hm);
     free(c);
 }
@@ -144,16 +143,12 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
             }
     }
     TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t)));
-    TRY(dev_alloc((void **)&c->d_deep_seg, (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * 4 * sizeof(uint32_t)));
-    c->giant_cap = 1u << 16;
-    TRY(dev_alloc((void **)&c->d_giant_list, c->giant_cap * sizeof(uint32_t)));
-    c->giant_keys = 1u << 20;
-    TRY(dev_alloc((void **)&c->d_giant_scratch,
-                  (size_t)SS_GIANT_BLOCKS * 2 * c->giant_keys * sizeof(uint32_t)));
+    TRY(dev_alloc((void **)&c->d_deep_seg, (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t)));
     TRY(dev_alloc((void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t)));
 #undef TRY
     if (hipMemset(c->d_counters, 0, 16 * sizeof(uint32_t)) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
         ss_ctx_destroy(c);
         return SS_E_HIP;
     }
@@ -221,20 +216,16 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     const uint64_t site_blocks = (b->n_sites + 15) / 16;
     const uint64_t wpb = SS_MAIN_BLOCK / 64;              /* waves per workgroup */
     uint64_t blocks = (site_blocks + wpb - 1) / wpb;
-    uint64_t per_cu = SS_MAIN_GRID_DEFAULT * 4 / wpb;     /* same waves per CU for any block size */
-    {   /* tuning experiments: workgroups per CU (d_deep_seg is sized for SS_MAIN_GRID_PER_CU) */
-        const char *g = getenv("SS_MAIN_GRID");
-        if (g && atoi(g) > 0 && (uint64_t)atoi(g) * wpb <= SS_MAIN_GRID_PER_CU * 4) per_cu = (uint64_t)atoi(g);
-    }
-    const uint64_t max_blocks = (uint64_t)c->n_cu * per_cu;
+    const uint64_t max_blocks = (uint64_t)c->n_cu * SS_MAIN_GRID_PER_CU;
     if (blocks > max_blocks) blocks = max_blocks;
     const uint64_t nseg = blocks * (SS_MAIN_BLOCK / 64);
     const uint64_t seg_cap = (site_blocks + nseg - 1) / nseg * 16;
     int rc = ensure_deep_cap(c, nseg * seg_cap);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    /* counters: giant, (err is sticky), scratch n_calls, scratch clamped, deep2 */
-    HIPCHK(hipMemsetAsync(c->d_counters, 0, 2 * sizeof(uint32_t), s));
+    /* one launch at a time per context (shared work lists and counters) */
+    if (c->launched && s != c->last_stream) HIPCHK(hipStreamWaitEvent(s, c->done, 0));
+    /* counters: deep2 (err is sticky until ss_ctx_check) */
     HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
@@ -258,16 +249,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.deep_cap = c->deep_cap;
     a.deep2_list = c->d_deep_list + c->deep_cap;
     a.deep2_count = c->d_counters + 5;
-    a.giant_list = c->d_giant_list;
-    a.giant_count = c->d_counters + 1;
-    a.giant_cap = c->giant_cap;
-    a.giant_scratch = c->d_giant_scratch;
-    a.giant_keys = c->giant_keys;
     a.err = c->d_counters + 2;
-    {   /* profiling ablations only (DESIGN.md "Measurement"); never set in production */
-        const char *dg = getenv("SS_DIAG");
-        a.diag = dg ? (uint32_t)strtoul(dg, nullptr, 0) : 0u;
-    }
     a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;
     {   /* only min(mapQ & 0x7f, cap) is ever used (sniper_maqcns.c:173) */
@@ -289,13 +271,12 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         evs = c->ev->data() + SS_EV_PER_LAUNCH * c->n_logged;
         ++c->n_logged;
     }
-    int wide_grid = c->n_cu;                      /* one 8-wave workgroup per CU fits (LDS) */
-    {   /* tuning experiments: rounds of wide workgroups per CU */
-        const char *g = getenv("SS_WIDE_GRID");
-        if (g && atoi(g) > 0 && atoi(g) <= 64) wide_grid = c->n_cu * atoi(g);
-    }
+    const int wide_grid = c->n_cu;                /* one 8-wave workgroup per CU fits (LDS) */
     int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, s, evs);
-    return e == 0 ? SS_OK : SS_E_HIP;
+    if (e != 0) return SS_E_HIP;
+    HIPCHK(hipEventRecord(c->done, s));
+    c->launched = 1;
+    return SS_OK;
 }
 
 extern "C" int ss_set_kernel_timing(ss_ctx_t *c, int enable)

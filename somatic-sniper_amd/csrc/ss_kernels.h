@@ -67,37 +67,21 @@ struct ss_score_args {
     uint32_t  *deep_seg_n;    /* [deep_nseg] entries each main wave wrote (every wave writes) */
     uint32_t   deep_seg_cap;
     uint32_t   deep_nseg;     /* = main-kernel waves */
-    uint32_t   deep_cap;      /* deep2 list capacity */
-    uint32_t  *deep2_list;    /* sites too deep for the wide kernel (ss_score_wide) */
+    uint32_t   deep_cap;      /* deep2 list capacity (>= n_sites: cannot overflow) */
+    uint32_t  *deep2_list;    /* sites the wide kernel cannot sort, any depth (ss_score_deep) */
     uint32_t  *deep2_count;
-    uint32_t  *giant_list;    /* sites deeper than the LDS limit of the deep kernel */
-    uint32_t  *giant_count;
-    uint32_t   giant_cap;
-    uint32_t  *giant_scratch; /* [giant_blocks][2][giant_keys] */
-    uint32_t   giant_keys;    /* keys per sample per giant block (power of two) */
     uint32_t  *err;           /* sticky error bits, see SS_KERR_* */
-    uint32_t   diag;          /* profiling ablations (SS_DIAG env), 0 in production */
     ss_dev_model m;
 };
 
-#define SS_KERR_DEEP_OVERFLOW  1u
-#define SS_KERR_GIANT_OVERFLOW 2u
-#define SS_KERR_TOO_DEEP       4u
-#define SS_KERR_MALFORMED      8u   /* decreasing read offsets: the site was not scored */
+#define SS_KERR_DEEP_OVERFLOW  1u   /* a deep list overflowed (cannot happen: sized from the batch) */
+#define SS_KERR_MALFORMED      8u   /* decreasing or out-of-range read offsets: the site scored -2 */
 
 /* Launch geometry constants shared with the host. */
-#ifndef SS_MAIN_BLOCK
 #define SS_MAIN_BLOCK      256   /* 4 waves                                    */
-#endif
-#define SS_MAIN_GRID_PER_CU 256  /* main-kernel workgroups per CU at most (deep-list segments) */
-#define SS_MAIN_GRID_DEFAULT 128 /* ... and by default: 4 resident, 32 rounds of short-lived waves (A/B: +5.5% over 16) */
-#define SS_MAIN_MAXN       256   /* per-sample depth handled by the main kernel */
+#define SS_MAIN_GRID_PER_CU 128  /* main-kernel workgroups per CU: 4 resident, 32 rounds of short-lived waves (+5.5% over 16) */
 #define SS_DEEP_BLOCK      256
-#define SS_DEEP_MAXN       4096  /* per-sample depth sorted in LDS by the deep kernel */
-#define SS_GIANT_BLOCKS    8
-#ifndef SS_WIDE_BLOCK
 #define SS_WIDE_BLOCK      512   /* 8 waves, one workgroup per CU (LDS)          */
-#endif
 #define SS_WIDE_MAXSLOTS   2048  /* sort slots (tumor + pad + normal) per site    */
 
 /* Launchers (return hipError_t as int). */

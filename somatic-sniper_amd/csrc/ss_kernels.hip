@@ -16,10 +16,12 @@
  *     10 genotype likelihoods between them, and lane s decides site s (gate,
  *     SNV candidate test, posteriors / joint prior, emit filter).  The DMA of
  *     the next sub-group overlaps the likelihood and decision phases.
- *   ss_score_deep   one 256-thread block per site with more than PK_MAX reads:
- *     block bitonic sort of 32-bit keys in LDS (<= SS_DEEP_MAXN per sample) or,
- *     for giant pileups, in a global scratch slice; then the same fold,
- *     likelihood and decision code (quad-cooperative variant).
+ *   ss_score_wide   sites with 513..2048 sort slots (the main kernel lists
+ *     them): the same packed network at 1024 / 2048 keys, 16 sites folded and
+ *     finished together.
+ *   ss_score_deep   one 256-thread block per site beyond that (any depth) or
+ *     with malformed offsets: counting sort of the order-relevant key fields
+ *     in LDS, then the same ordered fold, likelihood and decision code.
  *
  * Bit-exactness: built with -ffp-contract=off (no FMA contraction); float
  * division and double sqrt are correctly rounded (sqrt re-checked with fma);
@@ -28,56 +30,17 @@
 #include "ss_kernels.h"
 
 #define SENT 0xffffffffu
-#define GMAX 8              /* sites per group (deep kernel finish)  */
 
-/* kernel tuning switches (A/B builds: make variant DEFS=-D...) */
-#ifndef SS_XOR_BANK
-#define SS_XOR_BANK 1
-#endif
-#ifndef SS_SPLIT_SORT
-#define SS_SPLIT_SORT 1   /* skip the top merge level when each sample fits in half */
-#endif
-#ifndef SS_SPLIT_WIDE
-#define SS_SPLIT_WIDE SS_SPLIT_SORT
-#endif
-#ifndef SS_OPSEL
-#define SS_OPSEL 1        /* halfswaps folded into v_pk_min/max operand selects */
-#endif
-#ifndef SS_SWZ
-#define SS_SWZ 1          /* lane xor 16 / 31 through ds_swizzle instead of VALU permutes */
-#endif
-#ifndef SS_CX_EXEC
-#define SS_CX_EXEC 0      /* exec-masked max measured slower (SALU exec writes) */
-#endif
-#ifndef SS_PIN_COUNTS
-#define SS_PIN_COUNTS 1
-#endif
-#ifndef SS_ASM_HALVES
-#define SS_ASM_HALVES 1   /* in-register half compare-exchange as hand-written SDWA pairs */
-#endif
-#ifndef SS_FOLD_UNROLL
-#define SS_FOLD_UNROLL 8  /* fold loop unroll (A/B: 2 -> 8 is +0.5% main, +4% at 500x/500x) */
-#endif
+/* Fixed tuning of the shipped kernels (each measured on MI355X):
+ * one code path per choice, no run-time or build-time alternatives. */
+#define SS_FOLD_UNROLL 8  /* fold loop unroll (2 -> 8: +0.5% main, +4% at 500x/500x) */
+#define SS_PRIO_SORT 3    /* wave priority raised over the sort network (+1.8%) */
+#define SS_PRIO_WIDE 1    /* the same over the wide kernel's network (+3.7% at 500x/500x) */
 /* `#pragma unroll N` with N from a macro: the count reaches the pragma expanded */
 #define SS_PRAGMA(x) _Pragma(#x)
 #define SS_UNROLL(n) SS_PRAGMA(unroll n)
-#ifndef SS_PRIO_FOLD
-#define SS_PRIO_FOLD 0    /* wave priority raised over the fold's dependency chain */
-#endif
-#ifndef SS_PRIO_SORT
-#define SS_PRIO_SORT 3    /* wave priority raised over the sort network (A/B: +1.8%) */
-#endif
-#ifndef SS_GENO_BATCH
-#define SS_GENO_BATCH 3   /* likelihood gathers issued together, this many genotypes at a time (geno_p5; 0: one by one; 5 spills 12 B) */
-#endif
-#ifndef SS_WIDE_PREFETCH
-#define SS_WIDE_PREFETCH 1   /* wide kernel: next site's reads loaded into registers one site ahead */
-#endif
-#ifndef SS_PRIO_WIDE
-#define SS_PRIO_WIDE 1    /* the same over the wide kernel's network (A/B: +3.7% at 500x/500x) */
-#endif
 #ifndef SS_STAMP
-#define SS_STAMP 0        /* diagnostic builds: per-phase s_memtime cycle totals of the main kernel */
+#define SS_STAMP 0        /* profiling builds only (make variant): per-phase s_memtime cycle totals */
 #endif
 
 /* Phase stamps (SS_STAMP builds only): wave-uniform cycle accumulators,
@@ -145,83 +108,12 @@ __device__ __forceinline__ uint32_t wave_halfsums(uint32_t v)
     return v;
 }
 
-/* --------------------------------------------------------------------------
- * Order key of one packed read (sniper_maqcns.c:144-156 restated).
- *
- * The reference sorts  minq<<24 | hasbase<<21 | strand<<18 | nt4<<16 |
- * baseQ<<8 | mapQ  and folds in descending order, one accumulator per base.
- * Only the order WITHIN a base matters, and within a base nt4 is constant, so
- * we sort on  base<<26 | minq<<18 | hasbase<<17 | strand<<16 | baseQ<<8 | mapQ,
- * which yields each base's reads as one contiguous ascending run whose
- * descending walk is exactly the reference's sequence.  Reads whose clamped
- * quality q is 0 never touch esum/fsum/w/c (:165-172): they become SENT and
- * sort to the end.  rms (:173) is accumulated for every read.
- * ------------------------------------------------------------------------ */
-__device__ __forceinline__ uint32_t read_key(uint32_t rd, uint32_t ref16, uint32_t cap,
-                                             uint32_t &rms_term)
-{
-    const uint32_t mq = rd & 0xffu, bq = (rd >> 8) & 0xffu;
-    const uint32_t nt = (rd >> 16) & 0xfu, st = (rd >> 20) & 1u;
-    uint32_t t = mq & 0x7fu;
-    t = t < cap ? t : cap;
-    rms_term = t * t;
-    const uint32_t minq = mq < bq ? mq : bq;
-    const bool valid = minq != 0u || (bq & 0x3fu) != 0u;
-    const uint32_t nt4 = nt16_to_nt4(nt ? nt : ref16);
-    const uint32_t hb = nt4 < 4u ? 1u : 0u;
-    const uint32_t base = hb ? nt4 : 0u;  /* N / IUPAC count as A (Appendix A.1) */
-    return valid ? (base << 26 | minq << 18 | hb << 17 | st << 16 | bq << 8 | mq) : SENT;
-}
-
-/* per (site, sample) bookkeeping kept in LDS */
-struct SlotMeta {
-    uint32_t base;      /* arena offset of the sorted keys */
-    uint32_t start[4];  /* base group start (relative)      */
-    uint32_t cnt[4];    /* base group size == reference c[] before rescale */
-    uint32_t n;         /* non-deleted depth                */
-    uint32_t rms_lo, rms_hi;
-};
-
 struct SlotRes {
     uint8_t  lk[12];
     uint32_t cns;
     uint32_t depth;
     uint8_t  min_lk, rms_q, pad0, pad1;
 };
-
-struct SiteInfo {
-    uint32_t site;
-    uint32_t refc;
-};
-
-/* --------------------------------------------------------------------------
- * Phase B: ordered fold of one base group (sniper_maqcns.c:162-172).
- * keys: ascending run of the group; walked from the top.  fk from LDS.
- * ------------------------------------------------------------------------ */
-__device__ __forceinline__ void fold_group(const uint32_t *keys, uint32_t cnt, const double *fk,
-                                           float &es_out, float &fs_out)
-{
-    float es = 0.0f, fs = 0.0f;
-    uint32_t w0 = 0, w1 = 0;
-    uint32_t t = cnt;
-    uint32_t key = t ? keys[t - 1] : 0u;
-    while (t) {
-        --t;
-        const uint32_t cur = key;
-        if (t) key = keys[t - 1];            /* prefetch the next key */
-        const uint32_t minq = (cur >> 18) & 0xffu, bq = (cur >> 8) & 0xffu;
-        const uint32_t st = (cur >> 16) & 1u;
-        const uint32_t q = (minq < 4u && (bq & 0x3fu) != 0u) ? 4u : minq;
-        const uint32_t w = st ? w1 : w0;
-        const double f = fk[w];
-        es = (float)((double)es + f * (double)q);
-        fs = (float)((double)fs + f);
-        const uint32_t wn = w < 255u ? w + 1u : 255u;
-        if (st) w1 = wn; else w0 = wn;
-    }
-    es_out = es;
-    fs_out = fs;
-}
 
 /* correctly rounded sqrt of a non-negative double (re-checked with exact fma
  * residuals so the result does not depend on the library's rounding). */
@@ -350,21 +242,14 @@ __device__ __forceinline__ void geno_p_range(uint32_t role, const float es[4], c
     }
 }
 
-/* the five genotypes in batches of SS_GENO_BATCH (register pressure) */
+/* the five genotypes in batches of three and two (all five at once spills;
+ * one at a time waits once per genotype: -2.4%) */
 __device__ __forceinline__ void geno_p5(uint32_t role, const float es[4], const float fs[4],
                                         const uint32_t c[4], uint32_t tot, const ss_dev_model &m,
                                         float out[5])
 {
-    if constexpr (SS_GENO_BATCH >= 5) {
-        geno_p_range<0, 5>(role, es, fs, c, tot, m, out);
-    } else if constexpr (SS_GENO_BATCH >= 3) {
-        geno_p_range<0, 3>(role, es, fs, c, tot, m, out);
-        geno_p_range<3, 5>(role, es, fs, c, tot, m, out);
-    } else {
-        geno_p_range<0, 2>(role, es, fs, c, tot, m, out);
-        geno_p_range<2, 4>(role, es, fs, c, tot, m, out);
-        geno_p_range<4, 5>(role, es, fs, c, tot, m, out);
-    }
+    geno_p_range<0, 3>(role, es, fs, c, tot, m, out);
+    geno_p_range<3, 5>(role, es, fs, c, tot, m, out);
 }
 
 /* counts rescale of sniper_maqcns.c:178-182 */
@@ -594,64 +479,6 @@ __device__ __forceinline__ void store_glf(ss_glf_t *dst, uint32_t ref16, const u
 }
 
 /* --------------------------------------------------------------------------
- * Phases B + C + D for G sites whose slots are in LDS.  Called by every lane
- * of one wave.  keys_of(slot) gives the arena of that slot.
- * ------------------------------------------------------------------------ */
-template <typename KeysOf>
-__device__ __forceinline__ void finish_group(const ss_score_args &a, int G, const SlotMeta *meta,
-                                             SlotRes *res, const SiteInfo *sinfo,
-                                             const double *fk, KeysOf keys_of)
-{
-    const uint32_t lane = lane_id();
-    const int s = (int)(lane >> 3), slot = (int)(lane >> 2), b = (int)(lane & 3u);
-    float es = 0.0f, fs = 0.0f;
-    if (s < G) {
-        const SlotMeta &mt = meta[slot];
-        if (!(a.diag & 2u)) fold_group(keys_of(slot) + mt.start[b], mt.cnt[b], fk, es, fs);
-        else { es = (float)mt.cnt[b]; fs = es; }
-    }
-    /* gather the quad's four bases (all lanes active for the DPP moves) */
-    float E[4], F[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        E[i] = quad_bcast(es, i);
-        F[i] = quad_bcast(fs, i);
-    }
-    if (s < G) {
-        const SlotMeta &mt = meta[slot];
-        const uint32_t cnt[4] = {mt.cnt[0], mt.cnt[1], mt.cnt[2], mt.cnt[3]};
-        const uint64_t rms = (uint64_t)mt.rms_lo | (uint64_t)mt.rms_hi << 32;
-        uint32_t lk[10], min_lk, rms_q, cns;
-        if (!(a.diag & 4u)) glf_and_cns(b, E, F, cnt, mt.n, rms, a.m, lk, min_lk, rms_q, cns);
-        else {
-#pragma unroll
-            for (int g = 0; g < 10; ++g) lk[g] = (uint32_t)E[g & 3] & 0xffu;
-            min_lk = 0; rms_q = 0; cns = (uint32_t)F[0];
-        }
-        if (b == 0) {
-            SlotRes &r = res[slot];
-#pragma unroll
-            for (int g = 0; g < 10; ++g) r.lk[g] = (uint8_t)lk[g];
-            r.cns = cns;
-            r.depth = mt.n > 16777215u ? 16777215u : mt.n;
-            r.min_lk = (uint8_t)min_lk;
-            r.rms_q = (uint8_t)rms_q;
-            if (a.glf) {
-                const uint32_t site = sinfo[s].site;
-                const uint32_t ref16 = sinfo[s].refc >> 8;
-                store_glf(&a.glf[2ull * site + (slot & 1)], ref16, lk, min_lk, rms_q, r.depth);
-            }
-        }
-    }
-    wave_sync();
-    if ((int)lane < G) {
-        if (!(a.diag & 8u)) decide_site(a, sinfo[lane].site, sinfo[lane].refc, res[2 * lane], res[2 * lane + 1]);
-        else a.score[sinfo[lane].site] = (int32_t)res[2 * lane].cns;
-    }
-    wave_sync();
-}
-
-/* --------------------------------------------------------------------------
  * Main kernel.
  *
  * A wave walks 16-site BLOCKS (grid-strided).  A block's reads are contiguous
@@ -677,10 +504,7 @@ __device__ __forceinline__ void finish_group(const ss_score_args &a, int G, cons
  * then evaluates the 10 genotypes.  Phase D: lane s decides site s.
  * ------------------------------------------------------------------------ */
 #define GB 16               /* sites per block                 */
-#ifndef SS_STG
-#define SS_STG 2048
-#endif
-#define STG SS_STG          /* staged u32 per wave             */
+#define STG 2048            /* staged u32 per wave             */
 #define PK_MAX 512          /* nT + nN handled by the packed sort (K <= 4) */
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -702,7 +526,7 @@ struct MainLds {
     uint32_t refc[SS_MAIN_BLOCK / 64][GB];
 };
 
-/* 16-bit order key (see the section comment); 0xffff = no contribution.
+/* 16-bit order key (see the section comment); 0xffff = no contribution or pad.
  *   sample<<15 | base<<13 | minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz
  * E = baseQ >> 6 and nz = (baseQ & 0x3f) != 0 order the reads of one
  * (minq < 4, hasbase, strand) class exactly as the reference's baseQ tie-break
@@ -724,7 +548,10 @@ __device__ __forceinline__ uint32_t read_key16(uint32_t rd, uint32_t tb, uint32_
     const uint32_t E = __builtin_amdgcn_ubfe(rd, 14u, 2u);
     const uint32_t st = __builtin_amdgcn_ubfe(rd, 20u, 1u);
     const uint32_t key = samplebit | base << 13 | minq << 5 | hb << 4 | st << 3 | E << 1 | nz;
-    return (minq | lo6) != 0u ? key : 0xffffu;
+    /* a contributing normal read can have every field at its maximum (mapQ =
+     * baseQ = 255, T, reverse): 0xfffe keeps it below the pad key, and for
+     * minq >= 4 the E / nz bits only order reads of equal (q, strand) */
+    return (minq | lo6) != 0u ? min(key, 0xfffeu) : 0xffffu;
 }
 
 /* per-site base tables of read_key16 (bam_nt16_nt4_table semantics,
@@ -785,54 +612,36 @@ __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b)
  * not an instruction */
 __device__ __forceinline__ uint32_t pk_min_swo(uint32_t x, uint32_t o)
 {
-#if SS_OPSEL
     uint32_t r;
     asm("v_pk_min_u16 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(x), "v"(o));
     return r;
-#else
-    return pk_min(x, (o >> 16) | (o << 16));
-#endif
 }
 __device__ __forceinline__ uint32_t pk_max_swo(uint32_t x, uint32_t o)
 {
-#if SS_OPSEL
     uint32_t r;
     asm("v_pk_max_u16 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(x), "v"(o));
     return r;
-#else
-    return pk_max(x, (o >> 16) | (o << 16));
-#endif
 }
 /* halfswap(max(x, halfswap(o))) = max(halfswap(x), o) */
 __device__ __forceinline__ uint32_t pk_max_swx(uint32_t x, uint32_t o)
 {
-#if SS_OPSEL
     uint32_t r;
     asm("v_pk_max_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(x), "v"(o));
     return r;
-#else
-    return pk_max((x >> 16) | (x << 16), o);
-#endif
 }
 
-/* x from lane ^ LJ without an LDS round trip: DPP quad permutes for 1 and 2,
- * DPP row shifts for 4 and 8, v_permlane16/32_swap for 16 and 32. */
+/* x from lane ^ LJ: DPP quad permutes for 1 and 2, bank-masked DPP row
+ * shifts for 4 and 8, ds_swizzle for 16 and 31, v_permlane32_swap for 32,
+ * DPP mirrors for 3, 7 and 15. */
 
 template <int LJ>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
 {
     const int xi = (int)x;
-    /* SS_SWZ >= 2 / 3: more of the lane xors through the LDS crossbar
-     * (bit-mask mode, and 0x1f, xor LJ) -- trades VALU issue for LDS latency */
-    constexpr bool swz = (SS_SWZ >= 3 && (LJ == 1 || LJ == 2 || LJ == 3 || LJ == 7 || LJ == 15)) ||
-                         (SS_SWZ >= 2 && (LJ == 4 || LJ == 8));
-    if constexpr (swz) {
-        return (uint32_t)__builtin_amdgcn_ds_swizzle(xi, 0x1f | (LJ << 10));
-    } else if constexpr (LJ == 1) {
+    if constexpr (LJ == 1) {
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0xb1, 0xf, 0xf, false);  /* quad_perm 1,0,3,2 */
     } else if constexpr (LJ == 2) {
         return (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x4e, 0xf, 0xf, false);  /* quad_perm 2,3,0,1 */
-#if SS_XOR_BANK
     } else if constexpr (LJ == 4) {
         /* banks 0,2 read lane + 4, banks 1,3 lane - 4: two bank-masked moves
          * (the first one's other banks are don't-care: no zeroed old value) */
@@ -841,29 +650,11 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
     } else if constexpr (LJ == 8) {
         const int up = __builtin_amdgcn_mov_dpp(xi, 0x108, 0xf, 0x3, false);          /* row_shl:8 */
         return (uint32_t)__builtin_amdgcn_update_dpp(up, xi, 0x118, 0xf, 0xc, false); /* row_shr:8 */
-#else
-    } else if constexpr (LJ == 4) {
-        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x104, 0xf, 0xf, false); /* row_shl:4 */
-        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x114, 0xf, 0xf, false); /* row_shr:4 */
-        return (lane_id() & 4u) ? dn : up;
-    } else if constexpr (LJ == 8) {
-        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x108, 0xf, 0xf, false); /* row_shl:8 */
-        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp(xi, 0x118, 0xf, 0xf, false); /* row_shr:8 */
-        return (lane_id() & 8u) ? dn : up;
-#endif
-#if SS_SWZ
     } else if constexpr (LJ == 16) {
         /* ds_swizzle bit-mask mode (and 0x1f, xor 0x10): LDS crossbar, no VALU */
         return (uint32_t)__builtin_amdgcn_ds_swizzle(xi, 0x401f);
     } else if constexpr (LJ == 31) {
         return (uint32_t)__builtin_amdgcn_ds_swizzle(xi, 0x7c1f);                  /* xor 0x1f */
-#else
-    } else if constexpr (LJ == 16) {
-        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-        return (lane_id() & 16u) ? r[0] : r[1];
-    } else if constexpr (LJ == 31) {
-        return xor_lane<16>(xor_lane<15>(x));
-#endif
     } else if constexpr (LJ == 32) {
         const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
         return (lane_id() & 32u) ? r[0] : r[1];
@@ -879,48 +670,13 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
     }
 }
 
-
-
-/* Bitonic sort (the "flip" formulation: every comparator puts the minimum at
- * the lower index, so all directions are single lane bits), ascending, of
- * 128*K u16 keys: element e = lane*2K + 2r + h lives in half h of v[r]. */
-/* half cleaners e <-> e ^ j for j = J, J/2, ..., 1 (compile-time recursion);
- * M independent networks are advanced together so their dependency chains
- * (and DPP wait states) interleave. */
 /* Cross-lane compare-exchange of packed u16 pairs: lanes with bit LJ clear
- * keep min(x, o), lanes with it set keep max(x, o).  The max is issued under
- * an exec mask (2 VALU instead of min + max + select; no lane-mask SGPRs to
- * keep live across the network).  All lanes must be active on entry. */
+ * keep min(x, o), lanes with it set keep max(x, o).  (An exec-masked max,
+ * 2 VALU instead of 3, measured slower: SALU exec writes.) */
 template <int LJ>
 __device__ __forceinline__ uint32_t cx_lanes(uint32_t x, uint32_t o)
 {
-#if !SS_CX_EXEC
     return (lane_id() & (uint32_t)LJ) ? pk_max(x, o) : pk_min(x, o);
-#endif
-    uint32_t r;
-    uint64_t saved;
-    if constexpr (LJ == 32) {
-        asm volatile("v_pk_min_u16 %0, %2, %3\n\t"
-                     "s_mov_b64 %1, exec\n\t"
-                     "s_mov_b32 exec_lo, 0\n\t"
-                     "v_pk_max_u16 %0, %2, %3\n\t"
-                     "s_mov_b64 exec, %1"
-                     : "=&v"(r), "=&s"(saved)
-                     : "v"(x), "v"(o));
-    } else {
-        constexpr uint32_t pat = LJ == 1 ? 0xaaaaaaaau : LJ == 2 ? 0xccccccccu : LJ == 4 ? 0xf0f0f0f0u
-                               : LJ == 8 ? 0xff00ff00u : 0xffff0000u;
-        static_assert(LJ == 1 || LJ == 2 || LJ == 4 || LJ == 8 || LJ == 16, "lane bit");
-        asm volatile("v_pk_min_u16 %0, %2, %3\n\t"
-                     "s_mov_b64 %1, exec\n\t"
-                     "s_and_b32 exec_lo, exec_lo, %4\n\t"
-                     "s_and_b32 exec_hi, exec_hi, %4\n\t"
-                     "v_pk_max_u16 %0, %2, %3\n\t"
-                     "s_mov_b64 exec, %1"
-                     : "=&v"(r), "=&s"(saved)
-                     : "v"(x), "v"(o), "i"(pat));
-    }
-    return r;
 }
 
 /* In-register compare-exchange of the two halves: lo = min, hi = max, by two
@@ -930,10 +686,6 @@ __device__ __forceinline__ uint32_t cx_lanes(uint32_t x, uint32_t o)
  * (cx_halves2: two registers interleaved) or one wait state separates them. */
 __device__ __forceinline__ uint32_t cx_halves(uint32_t x)
 {
-#if !SS_ASM_HALVES
-    const uint32_t lo = x & 0xffffu, hi = x >> 16;
-    return min(lo, hi) | max(lo, hi) << 16;
-#endif
     uint32_t r;
     asm volatile("v_max_u16_sdwa %0, %1, %1 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
                  "s_nop 0\n\t"
@@ -945,11 +697,6 @@ __device__ __forceinline__ uint32_t cx_halves(uint32_t x)
 
 __device__ __forceinline__ void cx_halves2(uint32_t &x0, uint32_t &x1)
 {
-#if !SS_ASM_HALVES
-    x0 = cx_halves(x0);
-    x1 = cx_halves(x1);
-    return;
-#endif
     uint32_t r0, r1;
     asm volatile("v_max_u16_sdwa %0, %2, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
                  "v_max_u16_sdwa %1, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
@@ -971,6 +718,9 @@ __device__ __forceinline__ void halves_all(uint32_t (&v)[M][K])
     if constexpr (N & 1) v[M - 1][K - 1] = cx_halves(v[M - 1][K - 1]);
 }
 
+/* half cleaners e <-> e ^ j for j = J, J/2, ..., 1 (compile-time recursion);
+ * M independent networks are advanced together so their dependency chains
+ * (and DPP wait states) interleave. */
 template <int M, int K, uint32_t J>
 __device__ __forceinline__ void half_clean(uint32_t (&v)[M][K])
 {
@@ -1098,9 +848,7 @@ __device__ __forceinline__ uint32_t count_below(const uint32_t (&v)[K], uint32_t
         c += (uint32_t)__popcll(__ballot((v[r] & 0xffffu) < x));
         c += (uint32_t)__popcll(__ballot((v[r] >> 16) < x));
     }
-#if SS_PIN_COUNTS
     asm volatile("" : "+s"(c));
-#endif
     return c;
 }
 
@@ -1113,14 +861,14 @@ struct SiteA {
 
 template <int K, int M>
 __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M], uint32_t cap,
-                                           Slot3 *slot, uint32_t diag, Stamps &st)
+                                           Slot3 *slot, Stamps &st)
 {
     const uint32_t lane = lane_id();
     uint32_t v[M][K];
     uint32_t rs_t[M], rs_n[M];
     /* input placement (the two elements of a lane are adjacent reads of ONE
      * sample and come from LDS with one ds_read2; a pad element is invalid) */
-    bool split = SS_SPLIT_SORT != 0;
+    bool split = true;
 #pragma unroll
     for (int m = 0; m < M; ++m) split = split && split_fits<K>(S[m].nt, S[m].nn);
 #pragma unroll
@@ -1143,8 +891,8 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             const uint32_t lim = tum ? nt : nn;
             const uint32_t rd0 = stage[idx], rd1 = stage[idx + 1u];
             const uint32_t sb = tum ? 0u : 0x8000u;
-            uint32_t k0 = (diag & 16u) ? ((rd0 & 0x7fffu) | sb) : read_key16(rd0, tb, th, sb);
-            uint32_t k1 = (diag & 16u) ? ((rd1 & 0x7fffu) | sb) : read_key16(rd1, tb, th, sb);
+            uint32_t k0 = read_key16(rd0, tb, th, sb);
+            uint32_t k1 = read_key16(rd1, tb, th, sb);
             const bool in0 = i0 < lim, in1 = i0 + 1u < lim;
             k0 = in0 ? k0 : 0xffffu;
             k1 = in1 ? k1 : 0xffffu;
@@ -1159,7 +907,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
     }
     st.mark(7);
     if (SS_PRIO_SORT) __builtin_amdgcn_s_setprio(SS_PRIO_SORT);
-    if (!(diag & 1u)) packed_bitonic_flip<M, K>(v, !split);
+    packed_bitonic_flip<M, K>(v, !split);
     if (SS_PRIO_SORT) __builtin_amdgcn_s_setprio(0);
     st.mark(8);
     uint32_t *rec = stage;
@@ -1167,15 +915,10 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
     for (int m = 0; m < M; ++m) {
         const uint32_t nt = S[m].nt, nn = S[m].nn, bt = S[m].bt, bn = S[m].bn;
         /* group boundaries (sample, base) */
-        uint32_t c1, c2, c3, c4, c5, c6, c7, c8;
-        if (diag & 32u) {
-            c1 = 0; c2 = 0; c3 = 0; c4 = nt; c5 = nt; c6 = nt; c7 = nt; c8 = nt + nn;
-        } else {
-            c1 = count_below<K>(v[m], 1u << 13); c2 = count_below<K>(v[m], 2u << 13);
-            c3 = count_below<K>(v[m], 3u << 13); c4 = count_below<K>(v[m], 4u << 13);
-            c5 = count_below<K>(v[m], 5u << 13); c6 = count_below<K>(v[m], 6u << 13);
-            c7 = count_below<K>(v[m], 7u << 13); c8 = count_below<K>(v[m], 0xffffu);
-        }
+        const uint32_t c1 = count_below<K>(v[m], 1u << 13), c2 = count_below<K>(v[m], 2u << 13);
+        const uint32_t c3 = count_below<K>(v[m], 3u << 13), c4 = count_below<K>(v[m], 4u << 13);
+        const uint32_t c5 = count_below<K>(v[m], 5u << 13), c6 = count_below<K>(v[m], 6u << 13);
+        const uint32_t c7 = count_below<K>(v[m], 7u << 13), c8 = count_below<K>(v[m], 0xffffu);
         st.mark(9);
         /* fold records back over the staged reads: tumor run, normal run */
         if (split) {
@@ -1188,7 +931,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             for (int r = 0; r < K; ++r)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    if (e0 + 2u * r + (uint32_t)h < lim && !(diag & 64u))
+                    if (e0 + 2u * r + (uint32_t)h < lim)
                         rl0[2 * r + h] = key_to_rec((v[m][r] >> (16 * h)) & 0xffffu);
         } else {
 #pragma unroll
@@ -1198,7 +941,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
                     const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
                     const uint32_t key = (v[m][r] >> (16 * h)) & 0xffffu;
                     const bool tum = e < c4;
-                    if (e < c8 && !(diag & 64u)) {
+                    if (e < c8) {
                         const uint32_t idx = tum ? bt + e : bn + (e - c4);
                         rec[idx] = key_to_rec(key);
                     }
@@ -1207,10 +950,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
         }
         /* rms sums: split placement has one sample per half-wave */
         uint32_t rms_t, rms_n;
-        if (diag & 128u) {
-            rms_t = rs_t[m];
-            rms_n = rs_n[m];
-        } else if (split) {
+        if (split) {
             const uint32_t h = wave_halfsums(rs_n[m]);
             rms_t = (uint32_t)__builtin_amdgcn_readlane((int)h, 31);
             rms_n = (uint32_t)__builtin_amdgcn_readlane((int)h, 63);
@@ -1287,7 +1027,8 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
-/* lanes 0..16: off_t[s..s+16], 17..32: ref[s..s+15], 33..49: off_n[s..s+16] */
+/* lanes 0..16: off_t[s..s+16], 17..32: ref[s..s+15], 33..49: off_n[s..s+16],
+ * 50, 51: off_t[n_sites], off_n[n_sites] (the batch's read counts) */
 __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s)
 {
     /* The block's bases are wave-uniform (scalar registers); the lane offset is
@@ -1309,6 +1050,8 @@ __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s
         }
     } else if (lane < 50u) {
         if (lane - 33u <= rem) v = on[lane - 33u];
+    } else if (lane < 52u) {
+        v = (lane == 50u ? a.off_t : a.off_n)[a.n_sites];
     }
     return v;
 }
@@ -1321,6 +1064,16 @@ __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s
  * the mask of sites that need more sort slots than the packed main-kernel
  * sort (PK_MAX, incl. the pad element).  Recomputed where needed rather than
  * kept live across the block (register pressure). */
+/* a site the packed main-kernel sort cannot take: too many sort slots.  A
+ * decreasing offset (malformed batch) wraps one count to ~2^32, so each
+ * sample is also tested on its own: such sites go down the deep lists, whose
+ * kernel scores them -2 without a read load. */
+__device__ __forceinline__ bool off_packed(uint32_t t0, uint32_t t1, uint32_t n0, uint32_t n1)
+{
+    const uint32_t nt = t1 - t0, nn = n1 - n0;
+    return nt + (nt & 1u) + nn > PK_MAX || max(nt, nn) > PK_MAX;
+}
+
 struct BlockScan {
     uint32_t incl;        /* per lane: reads of sites 0..lane */
     uint64_t deep;        /* wave-uniform */
@@ -1334,13 +1087,11 @@ __device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
      * permlane32 swap, then one more wave_shl:1 (no LDS address register) */
     const auto sw = __builtin_amdgcn_permlane32_swap(desc, desc, false, false);
     const uint32_t n0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sw[1], 0x130, 0xf, 0xf, false);
-    const uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)desc, 0x130, 0xf, 0xf, false) - desc;
-    const uint32_t nn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n0, 0x130, 0xf, 0xf, false) - n0;
-    const uint32_t sz = lane < nsite ? nt + nn : 0u;
+    const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)desc, 0x130, 0xf, 0xf, false);
+    const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n0, 0x130, 0xf, 0xf, false);
+    const uint32_t sz = lane < nsite ? (t1 - desc) + (n1 - n0) : 0u;
     BlockScan r;
-    /* a decreasing offset (malformed batch) wraps one count to ~2^32: the
-     * per-sample test keeps such a site off the packed path whatever the sum */
-    r.deep = __ballot(lane < nsite && (sz + (nt & 1u) > PK_MAX || max(nt, nn) > PK_MAX));
+    r.deep = __ballot(lane < nsite && off_packed(desc, t1, n0, n1));
     int x = (int)sz;
     x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);    /* row_shr:1 */
     x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);    /* row_shr:2 */
@@ -1350,17 +1101,28 @@ __device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
     return r;
 }
 
-/* Hand every site of the block that is too deep for the packed sort to the
- * wide kernel: one list push per block, not per site. */
-__device__ __forceinline__ void push_block_deep(const ss_score_args &a, uint32_t desc, uint32_t nsite,
-                                                uint64_t sblk, uint32_t *seg, uint32_t &ndeep)
+/* A block becomes current: its offsets are clamped to the batch's read
+ * count (descriptor lanes 50 / 51 hold off_t[n], off_n[n]; an offset past it
+ * can only come with a decreasing one later, so the batch is flagged
+ * malformed, and no load ever leaves the reads), then every site too deep for
+ * the packed sort is handed to the wide kernel: one list push per block. */
+__device__ __forceinline__ void begin_block(const ss_score_args &a, uint32_t &desc, uint32_t nsite,
+                                            uint64_t sblk, uint32_t *seg, uint32_t &ndeep)
 {
     const uint32_t lane = lane_id();
+    {
+        const uint32_t end = lane < 17u ? rl(desc, 50u) : rl(desc, 51u);
+        const bool off_lane = lane < 17u || (lane >= 33u && lane < 50u);
+        const bool past = off_lane && desc > end;
+        if (__ballot(past)) {
+            if (lane == 0) atomicOr(a.err, SS_KERR_MALFORMED);
+            desc = past ? end : desc;
+        }
+    }
     const int i = (int)(lane & 15u);
     const uint32_t t0 = (uint32_t)__shfl((int)desc, i), t1 = (uint32_t)__shfl((int)desc, i + 1);
     const uint32_t n0 = (uint32_t)__shfl((int)desc, 33 + i), n1 = (uint32_t)__shfl((int)desc, 34 + i);
-    const uint32_t nt = t1 - t0;
-    const bool deep = lane < nsite && (nt + (nt & 1u) + (n1 - n0)) > PK_MAX;
+    const bool deep = lane < nsite && off_packed(t0, t1, n0, n1);
     const uint64_t mask = __ballot(deep);
     if (mask == 0) return;
     if (deep) {
@@ -1436,7 +1198,7 @@ template <typename RecT>
 __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const RecT *recs, uint32_t *stage,
                                            const Slot3 *slot, SlotRes *res, const uint32_t *sites,
                                            const uint32_t *refcs, const double *fk,
-                                           bool have_next, const Sub &nxt, uint32_t diag, Stamps &st)
+                                           bool have_next, const Sub &nxt, Stamps &st)
 {
     const uint32_t lane = lane_id();
     const int sl = (int)(lane >> 1);               /* slot = site * 2 + sample */
@@ -1451,14 +1213,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         depth = m3.rec_n >> 16;
         rms = m3.rms;
         const RecT *rec = recs + (m3.rec_n & 0xffffu);
-        if (SS_PRIO_FOLD) __builtin_amdgcn_s_setprio(SS_PRIO_FOLD);
-        if (!(diag & 2u)) {
-            fold_sample<RecT>(rec, cnt, fk, role, acc);
-        } else {
-#pragma unroll
-            for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b];
-        }
-        if (SS_PRIO_FOLD) __builtin_amdgcn_s_setprio(0);
+        fold_sample<RecT>(rec, cnt, fk, role, acc);
     } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
@@ -1484,18 +1239,9 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     uint32_t c[4];
     const uint32_t tot = rescale_counts(cnt, c);
     float mine[5];
-    if (SS_GENO_BATCH > 0) {
-        geno_p5(role, es, fs, c, tot, a.m, mine);
+    geno_p5(role, es, fs, c, tot, a.m, mine);
 #pragma unroll
-        for (int t = 0; t < 5; ++t) mine[t] = (act && !(diag & 4u)) ? mine[t] : 0.0f;
-    } else {
-#pragma unroll
-        for (int t = 0; t < 5; ++t) {
-            int j, k;
-            geno_jk((int)role * 5 + t, j, k);
-            mine[t] = (act && !(diag & 4u)) ? geno_p(j, k, es, fs, c, tot, a.m) : 0.0f;
-        }
-    }
+    for (int t = 0; t < 5; ++t) mine[t] = act ? mine[t] : 0.0f;
     float p[10];
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
@@ -1506,12 +1252,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     st.mark(12);
     if (act && role == 0u) {
         uint32_t lk[10], min_lk, rms_q, cns;
-        if (!(diag & 4u)) glf_finish(p, es, depth, rms, a.m, lk, min_lk, rms_q, cns);
-        else {
-#pragma unroll
-            for (int g = 0; g < 10; ++g) lk[g] = (uint32_t)es[g & 3] & 0xffu;
-            min_lk = 0; rms_q = 0; cns = (uint32_t)fs[0];
-        }
+        glf_finish(p, es, depth, rms, a.m, lk, min_lk, rms_q, cns);
         SlotRes &r = res[sl];
         uint32_t *rw = reinterpret_cast<uint32_t *>(r.lk);
         rw[0] = lk[0] | lk[1] << 8 | lk[2] << 16 | lk[3] << 24;
@@ -1527,31 +1268,22 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     }
     wave_sync();
     st.mark(4);
-    if ((int)lane < G) {
-        /* the decision reads both samples' records straight from LDS */
-        if (!(diag & 8u)) decide_site(a, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
-        else a.score[sites[lane]] = (int32_t)res[2 * lane].cns;
-    }
+    /* the decision reads both samples' records straight from LDS */
+    if ((int)lane < G) decide_site(a, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
     wave_sync();
     st.mark(5);
 }
 
 }  // namespace
 
-/* DIAG = true only for the profiling ablations (SS_DIAG); the production
- * instance has every ablation branch folded away. */
-template <bool DIAG>
-#ifndef SS_MAIN_OCC
-#define SS_MAIN_OCC 4     /* waves per SIMD the main kernel is compiled for (VGPR budget) */
-#endif
-__global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(SS_MAIN_OCC)))
+/* compiled for 4 waves per SIMD (the VGPR and the LDS budget both allow 4) */
+__global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
 void ss_score_main(ss_score_args a)
 {
-    const uint32_t diag = DIAG ? a.diag : 0u;
     __shared__ double fk[256];
     __shared__ MainLds L;
     const uint32_t lane = lane_id();
-    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   /* wave-uniform */
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
     Stamps st;
@@ -1579,7 +1311,7 @@ void ss_score_main(ss_score_args a)
     uint32_t nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
     uint64_t nblk = blk + nwaves;
     uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-    push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
+    begin_block(a, desc, nsite, blk * GB, seg, ndeep);
     Sub cur = form_sub(desc, nsite, 0);
     while (cur.a == cur.b) {               /* whole block deep */
         blk = nblk;
@@ -1592,7 +1324,7 @@ void ss_score_main(ss_score_args a)
         nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
         nblk = blk + nwaves;
         ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-        push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
+        begin_block(a, desc, nsite, blk * GB, seg, ndeep);
         cur = form_sub(desc, nsite, 0);
     }
     issue_dma(a, cur, stage);
@@ -1623,16 +1355,16 @@ void ss_score_main(ss_score_args a)
                 }
             }
             if (i + 1u < cur.b && tot[0] <= 256u && tot[1] <= 256u) {   /* two sites, interleaved */
-                if (tot[0] <= 128u && tot[1] <= 128u) sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, diag, st);
-                else sort_sites<2, 2>(stage, S2, cap, slot + 2 * G, diag, st);
+                if (tot[0] <= 128u && tot[1] <= 128u) sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, st);
+                else sort_sites<2, 2>(stage, S2, cap, slot + 2 * G, st);
                 G += 2;
                 i += 2;
                 continue;
             }
             SiteA S1[1] = {S2[0]};
-            if (tot[0] <= 128u) sort_sites<1, 1>(stage, S1, cap, slot + 2 * G, diag, st);
-            else if (tot[0] <= 256u) sort_sites<2, 1>(stage, S1, cap, slot + 2 * G, diag, st);
-            else sort_sites<4, 1>(stage, S1, cap, slot + 2 * G, diag, st);
+            if (tot[0] <= 128u) sort_sites<1, 1>(stage, S1, cap, slot + 2 * G, st);
+            else if (tot[0] <= 256u) sort_sites<2, 1>(stage, S1, cap, slot + 2 * G, st);
+            else sort_sites<4, 1>(stage, S1, cap, slot + 2 * G, st);
             ++G;
             ++i;
         }
@@ -1652,13 +1384,13 @@ void ss_score_main(ss_score_args a)
             nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
             nblk = blk + nwaves;
             ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-            push_block_deep(a, desc, nsite, blk * GB, seg, ndeep);
+            begin_block(a, desc, nsite, blk * GB, seg, ndeep);
             nxt = form_sub(desc, nsite, 0);
             have = nxt.a < nxt.b;
         }
         st.mark(2);
         /* ---- phases B + C + D (the next DMA is issued after the fold) ---- */
-        finish_sub<uint32_t>(a, G, stage, stage, slot, res, sites, refcs, fk, have, nxt, diag, st);
+        finish_sub<uint32_t>(a, G, stage, stage, slot, res, sites, refcs, fk, have, nxt, st);
         if (!have) break;
         cur = nxt;
     }
@@ -1683,10 +1415,8 @@ void ss_score_main(ss_score_args a)
 namespace {
 
 #define WIDE_WAVES (SS_WIDE_BLOCK / 64)
-#ifndef SS_WIDE_LDS_U16
-#define SS_WIDE_LDS_U16 73728              /* u16 fold records per workgroup: 144 KB of LDS */
-#endif
-#define WIDE_ARENA (SS_WIDE_LDS_U16 / WIDE_WAVES)   /* per wave */
+#define WIDE_LDS_U16 73728                 /* u16 fold records per workgroup: 144 KB of LDS */
+#define WIDE_ARENA (WIDE_LDS_U16 / WIDE_WAVES)      /* per wave */
 
 struct WideLds {
     uint16_t arena[WIDE_WAVES][WIDE_ARENA];
@@ -1704,14 +1434,15 @@ struct WideSite {
     uint32_t ot, nt, on, nn;
     uint32_t ref;      /* ref char | nt16 code << 8, loaded with the offsets (one site ahead) */
     bool split;        /* split placement (see split_fits): top level skipped */
-    bool over;         /* more than SS_WIDE_MAXSLOTS slots (or a wrapped count): deep kernel */
+    bool over;         /* more than SS_WIDE_MAXSLOTS slots or malformed offsets: deep kernel */
 };
 
-__device__ __forceinline__ void wide_place(WideSite &w)
+__device__ __forceinline__ void wide_place(WideSite &w, uint32_t end_t, uint32_t end_n)
 {
-    w.over = max(w.nt, w.nn) > SS_WIDE_MAXSLOTS || w.nt + (w.nt & 1u) + w.nn > SS_WIDE_MAXSLOTS;
+    w.over = max(w.nt, w.nn) > SS_WIDE_MAXSLOTS || w.nt + (w.nt & 1u) + w.nn > SS_WIDE_MAXSLOTS ||
+             w.ot + w.nt < w.ot || w.ot + w.nt > end_t || w.on + w.nn < w.on || w.on + w.nn > end_n;
     const bool k8 = w.nt + (w.nt & 1u) + w.nn <= 1024u;      /* the network sort_site_wide picks */
-    w.split = SS_SPLIT_WIDE != 0 && (k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn));
+    w.split = k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn);
 }
 
 __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite &w, uint32_t (&rd)[32])
@@ -1794,13 +1525,14 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
     const uint32_t lane = lane_id();
-    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   /* wave-uniform */
     uint16_t *arena = L.arena[wv];
     Slot3 *slot = L.slot[wv];
     SlotRes *res = L.res[wv];
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const Sub none = {0, 0, 0, 0, 0, 0};
+    const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
     /* the main kernel's per-wave segments, GB entries at a time */
     for (uint32_t sg = blockIdx.x * WIDE_WAVES + wv; sg < a.deep_nseg; sg += gridDim.x * WIDE_WAVES)
     for (uint32_t first = 0, scount = min(a.deep_seg_n[sg], a.deep_seg_cap); first < scount; first += GB) {
@@ -1818,11 +1550,11 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
             w.nn = a.off_n[s + 1] - w.on;
             const uint32_t rc = a.ref[s];
             w.ref = rc | (uint32_t)ss_tab_nt16(a.m)[rc] << 8;
-            wide_place(w);
+            wide_place(w, end_t, end_n);
         };
         if (nlist) {
             describe(0, s_cur, w_cur);
-            if (SS_WIDE_PREFETCH) wide_load(a, w_cur, rd);
+            wide_load(a, w_cur, rd);
         }
         while (i < nlist) {
             int G = 0;
@@ -1833,15 +1565,11 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
                 if (used + slots > WIDE_ARENA && !w.over) break;   /* next sub-group */
                 uint32_t cur[32];
-                if (SS_WIDE_PREFETCH) {
 #pragma unroll
-                    for (int k = 0; k < 32; ++k) cur[k] = rd[k];
-                } else {
-                    wide_load(a, w, cur);
-                }
+                for (int k = 0; k < 32; ++k) cur[k] = rd[k];
                 if (i + 1 < nlist) {
                     describe(i + 1, s_cur, w_cur);
-                    if (SS_WIDE_PREFETCH) wide_load(a, w_cur, rd);
+                    wide_load(a, w_cur, rd);
                 }
                 ++i;
                 if (w.over) {
@@ -1866,129 +1594,193 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
             }
             wave_sync();
             Stamps nost;
-            if (G) finish_sub<uint16_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, 0u, nost);
+            if (G) finish_sub<uint16_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, nost);
         }
     }
 }
 
 /* --------------------------------------------------------------------------
- * Deep kernel: one block per site whose deeper sample exceeds SS_MAIN_MAXN.
- * GIANT = false: LDS sort (<= SS_DEEP_MAXN per sample), deeper sites are
- * forwarded to the giant list.  GIANT = true: a global scratch slice per block.
+ * Deep kernel: the sites the wide kernel cannot sort (more than
+ * SS_WIDE_MAXSLOTS sort slots, any depth) and sites with malformed offsets.
+ *
+ * No sort: the fold only needs each (sample, base) group's reads in the
+ * reference's descending key order (sniper_maqcns.c:157-172), and reads with
+ * equal (q, strand) contribute identical terms (see read_key16), so a
+ * counting sort over the order-relevant key fields is exact.  Bins of one
+ * base group, ascending in key order (DBIN per group):
+ *   minq <  4:  minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz        0..127
+ *   minq >= 4:  128 + (minq - 4) * 4 + hasbase * 2 + strand         128..1135
+ * (for minq >= 4, E and nz only order reads of equal q and strand).
+ * One 256-thread block per site builds both samples' histograms in LDS
+ * (36 KB) and an occupancy bitmap; then 16 lanes of wave 0 -- (sample, base,
+ * role) -- walk their group's bins from the top through the bitmap, folding
+ * count-many steps per bin: the reference's serial chain, O(depth), with no
+ * depth limit and no scratch memory.  The quads then evaluate the genotype
+ * likelihoods and lane 0 decides the site.
  * ------------------------------------------------------------------------ */
 namespace {
 
-__device__ void block_bitonic(uint32_t *buf, uint32_t P)
-{
-    for (uint32_t k = 2; k <= P; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < (P >> 1); t += blockDim.x) {
-                const uint32_t i = ((t & ~(j - 1u)) << 1) | (t & (j - 1u));
-                const uint32_t p = i | j;
-                const bool up = (i & k) == 0u;
-                const uint32_t x = buf[i], y = buf[p];
-                if ((x > y) == up) { buf[i] = y; buf[p] = x; }
-            }
-            __syncthreads();
-        }
-}
+#define DBIN 1136
+#define DBINS (2 * 4 * DBIN)
+#define DWORDS (DBINS / 32)
+static_assert(DBINS % 32 == 0, "bitmap words");
 
 struct DeepLds {
-    SlotMeta meta[2];
-    SlotRes res[2];
-    SiteInfo sinfo[1];
-    uint32_t cnt[2][4];
+    uint32_t hist[DBINS];
+    uint32_t occ[DWORDS];
     unsigned long long rms[2];
+    SlotRes res[2];
 };
 
-/* block-wide sort of one sample into buf; fills meta (thread 0) */
-__device__ void deep_sample(const uint32_t *reads, uint32_t n, uint32_t ref16, uint32_t cap,
-                            uint32_t *buf, DeepLds &D, int m)
+/* bin of one packed read within its sample's histogram, or SENT when its
+ * clamped q is 0 (no contribution, sniper_maqcns.c:165-166) */
+__device__ __forceinline__ uint32_t deep_bin(uint32_t rd, uint32_t tb, uint32_t th)
 {
-    uint32_t P = 64;
-    while (P < n) P <<= 1;
-    if (threadIdx.x < 4) D.cnt[m][threadIdx.x] = 0;
-    if (threadIdx.x == 0) D.rms[m] = 0ull;
-    __syncthreads();
-    unsigned long long rs = 0;
-    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-        uint32_t t = 0, v = SENT;
-        if (i < n) { v = read_key(reads[i], ref16, cap, t); rs += t; }
-        buf[i] = v;
+    const uint32_t bq = (rd >> 8) & 0xffu;
+    const uint32_t minq = min(rd & 0xffu, bq);
+    const uint32_t nz = (bq & 0x3fu) != 0u ? 1u : 0u;
+    const uint32_t nt2 = (rd >> 15) & 0x1eu;
+    const uint32_t base = __builtin_amdgcn_ubfe(tb, nt2, 2u);
+    const uint32_t hb = __builtin_amdgcn_ubfe(th, nt2, 1u);
+    const uint32_t st = (rd >> 20) & 1u;
+    const uint32_t idx = minq < 4u ? (minq << 5 | hb << 4 | st << 3 | (bq >> 6) << 1 | nz)
+                                   : 128u + (minq - 4u) * 4u + hb * 2u + st;
+    return (minq | nz) != 0u ? base * DBIN + idx : SENT;
+}
+
+/* offsets of a site are usable iff they neither decrease nor pass the end of
+ * the batch's reads (a malformed batch must not steer a load anywhere else) */
+__device__ __forceinline__ bool site_wellformed(uint32_t o0, uint32_t o1, uint32_t end)
+{
+    return o0 <= o1 && o1 <= end;
+}
+
+/* histogram one sample's reads; returns this thread's rms partial sum */
+__device__ __forceinline__ uint64_t deep_hist(const uint32_t *reads, uint32_t n, uint32_t tb, uint32_t th,
+                                              uint32_t cap, uint32_t *hist)
+{
+    uint64_t rs = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t rd = __builtin_nontemporal_load(reads + i);
+        const uint32_t b = deep_bin(rd, tb, th);
+        if (b != SENT) atomicAdd(&hist[b], 1u);
+        const uint32_t t = min(rd & 0x7fu, cap);
+        rs += t * t;
     }
-    atomicAdd(&D.rms[m], rs);
-    __syncthreads();
-    block_bitonic(buf, P);
-    uint32_t c[4] = {0, 0, 0, 0};
-    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-        const uint32_t v = buf[i];
-        if (v != SENT) ++c[v >> 26];
+    return rs;
+}
+
+/* ordered fold of one (sample, base) group from its histogram: acc gets
+ * esum (role 0) or fsum (role 1), cnt the group size c[] (sniper_maqcns.c:160-172) */
+__device__ __forceinline__ void deep_fold(const uint32_t *hist, const uint32_t *occ, uint32_t lo,
+                                          const double *fk, uint32_t role, float &acc, uint32_t &cnt)
+{
+    float e = 0.0f;
+    uint32_t w0 = 0, w1 = 0, c = 0;
+    const uint32_t hi = lo + DBIN;                 /* bins [lo, hi), walked downwards */
+    for (int wi = (int)((hi - 1u) >> 5); wi >= (int)(lo >> 5); --wi) {
+        uint32_t bits = occ[wi];
+        const uint32_t b0 = (uint32_t)wi * 32u;
+        if (b0 < lo) bits &= ~0u << (lo - b0);
+        if (b0 + 32u > hi) bits &= ~0u >> (b0 + 32u - hi);
+        while (bits) {
+            const uint32_t j = 31u - (uint32_t)__builtin_clz(bits);
+            bits &= ~(1u << j);
+            const uint32_t idx = b0 + j - lo;
+            const uint32_t k = hist[b0 + j];
+            const uint32_t q = idx < 128u ? max(idx >> 5, (idx & 1u) << 2) : (idx - 128u) / 4u + 4u;
+            const uint32_t st = idx < 128u ? (idx >> 3) & 1u : idx & 1u;
+            const double mul = role ? 1.0 : (double)q;
+            uint32_t w = st ? w1 : w0;
+            for (uint32_t r = 0; r < k; ++r) {
+                e = (float)((double)e + fk[w] * mul);
+                w = w < 255u ? w + 1u : 255u;
+            }
+            if (st) w1 = w; else w0 = w;
+            c += k;
+        }
     }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) if (c[b]) atomicAdd(&D.cnt[m][b], c[b]);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        SlotMeta &mt = D.meta[m];
-        uint32_t acc = 0;
-        for (int b = 0; b < 4; ++b) { mt.start[b] = acc; mt.cnt[b] = D.cnt[m][b]; acc += D.cnt[m][b]; }
-        mt.base = 0;
-        mt.n = n;
-        mt.rms_lo = (uint32_t)D.rms[m];
-        mt.rms_hi = (uint32_t)(D.rms[m] >> 32);
-    }
+    acc = e;
+    cnt = c;
 }
 
 }  // namespace
 
-template <bool GIANT>
 __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
 {
     __shared__ double fk[256];
     __shared__ DeepLds D;
-    __shared__ uint32_t lbuf[GIANT ? 1 : 2][GIANT ? 1 : SS_DEEP_MAXN];
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
-    const uint32_t count = GIANT ? *a.giant_count : *a.deep2_count;
-    const uint32_t lim = GIANT ? (count < a.giant_cap ? count : a.giant_cap)
-                               : (count < a.deep_cap ? count : a.deep_cap);
-    const uint32_t *list = GIANT ? a.giant_list : a.deep2_list;
-    uint32_t *bt, *bn;
-    if (GIANT) {
-        bt = a.giant_scratch + (size_t)blockIdx.x * 2u * a.giant_keys;
-        bn = bt + a.giant_keys;
-    } else {
-        bt = lbuf[0];
-        bn = lbuf[GIANT ? 0 : 1];
-    }
-    const uint32_t maxn = GIANT ? a.giant_keys : (uint32_t)SS_DEEP_MAXN;
+    const uint32_t count = *a.deep2_count;
+    const uint32_t lim = count < a.deep_cap ? count : a.deep_cap;
+    const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
+    const uint32_t lane = lane_id();
     for (uint32_t w = blockIdx.x; w < lim; w += gridDim.x) {
-        const uint32_t s = list[w];
-        const uint32_t ot = a.off_t[s], nt = a.off_t[s + 1] - ot;
-        const uint32_t on = a.off_n[s], nn = a.off_n[s + 1] - on;
-        if (nt > maxn || nn > maxn) {
+        const uint32_t s = a.deep2_list[w];
+        const uint32_t ot = a.off_t[s], ot1 = a.off_t[s + 1], on = a.off_n[s], on1 = a.off_n[s + 1];
+        if (!site_wellformed(ot, ot1, end_t) || !site_wellformed(on, on1, end_n)) {
             if (threadIdx.x == 0) {
-                if (!GIANT) {
-                    const uint32_t d = atomicAdd(a.giant_count, 1u);
-                    if (d < a.giant_cap) a.giant_list[d] = s;
-                    else atomicOr(a.err, SS_KERR_GIANT_OVERFLOW);
-                } else {
-                    /* a count >= 2^31 can only come from decreasing offsets */
-                    atomicOr(a.err, ((nt | nn) & 0x80000000u) ? SS_KERR_MALFORMED : SS_KERR_TOO_DEEP);
-                    a.score[s] = -2;
-                }
+                atomicOr(a.err, SS_KERR_MALFORMED);
+                a.score[s] = -2;
             }
-            continue;
+            continue;                                  /* block-uniform */
         }
+        const uint32_t nt = ot1 - ot, nn = on1 - on;
         const uint32_t refc = a.ref[s];
         const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
-        if (threadIdx.x == 0) { D.sinfo[0].site = s; D.sinfo[0].refc = refc | ref16 << 8; }
-        deep_sample(a.reads_t + ot, nt, ref16, cap, bt, D, 0);
-        deep_sample(a.reads_n + on, nn, ref16, cap, bn, D, 1);
+        uint32_t tb, th;
+        nt_tables(ref16, tb, th);
+        for (uint32_t i = threadIdx.x; i < DBINS; i += blockDim.x) D.hist[i] = 0u;
+        if (threadIdx.x < 2u) D.rms[threadIdx.x] = 0ull;
         __syncthreads();
-        if (threadIdx.x < 64)
-            finish_group(a, 1, D.meta, D.res, D.sinfo, fk,
-                         [&](int slot) -> const uint32_t * { return slot ? bn : bt; });
+        const uint64_t rt = deep_hist(a.reads_t + ot, nt, tb, th, cap, D.hist);
+        const uint64_t rn = deep_hist(a.reads_n + on, nn, tb, th, cap, D.hist + 4 * DBIN);
+        atomicAdd(&D.rms[0], (unsigned long long)rt);
+        atomicAdd(&D.rms[1], (unsigned long long)rn);
+        __syncthreads();
+        for (uint32_t wd = threadIdx.x; wd < DWORDS; wd += blockDim.x) {
+            uint32_t bits = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 32u; ++j) bits |= (D.hist[wd * 32u + j] != 0u ? 1u : 0u) << j;
+            D.occ[wd] = bits;
+        }
+        __syncthreads();
+        if (threadIdx.x < 64u) {
+            /* fold lanes 0..15: sample = lane >> 3, base = (lane >> 1) & 3, role = lane & 1 */
+            float acc = 0.0f;
+            uint32_t cnt = 0;
+            if (lane < 16u)
+                deep_fold(D.hist, D.occ, ((lane >> 3) * 4u + ((lane >> 1) & 3u)) * DBIN, fk, lane & 1u, acc, cnt);
+            /* lanes 0..3 finish the tumor, 4..7 the normal (quad-cooperative) */
+            const uint32_t smp = (lane >> 2) & 1u;
+            float es[4], fs[4];
+            uint32_t c[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int src = (int)(smp * 8u + 2u * (uint32_t)b);
+                es[b] = __shfl(acc, src);
+                fs[b] = __shfl(acc, src + 1);
+                c[b] = (uint32_t)__shfl((int)cnt, src);
+            }
+            const uint32_t n = smp ? nn : nt;
+            const uint64_t rms = D.rms[smp];
+            uint32_t lk[10], min_lk, rms_q, cns;
+            glf_and_cns((int)(lane & 3u), es, fs, c, n, rms, a.m, lk, min_lk, rms_q, cns);
+            if (lane == 0u || lane == 4u) {
+                SlotRes &r = D.res[smp];
+#pragma unroll
+                for (int g = 0; g < 10; ++g) r.lk[g] = (uint8_t)lk[g];
+                r.cns = cns;
+                r.depth = n > 16777215u ? 16777215u : n;
+                r.min_lk = (uint8_t)min_lk;
+                r.rms_q = (uint8_t)rms_q;
+                if (a.glf) store_glf(&a.glf[2ull * s + smp], ref16, lk, min_lk, rms_q, r.depth);
+            }
+            wave_sync();
+            if (lane == 0u) decide_site(a, s, refc | ref16 << 8, D.res[0], D.res[1]);
+        }
         __syncthreads();
     }
 }
@@ -2037,16 +1829,13 @@ int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int de
 {
     hipError_t e;
     if (ev) (void)hipEventRecord(ev[0], s);
-    if (a.diag) hipLaunchKernelGGL(ss_score_main<true>, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
-    else hipLaunchKernelGGL(ss_score_main<false>, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(ss_score_main, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(ss_score_wide, dim3(wide_grid), dim3(SS_WIDE_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[2], s);
-    hipLaunchKernelGGL(ss_score_deep<false>, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(ss_score_deep<true>, dim3(SS_GIANT_BLOCKS), dim3(SS_DEEP_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(ss_score_deep, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[3], s);
     return (int)hipSuccess;

@@ -68,16 +68,17 @@ def test_synthetic_parity(pkg, oracle, lt, ln, kw, opts):
 @pytest.mark.parametrize("lt,ln,fixed,n", [(300, 300, 0, 300), (700, 700, 1, 60), (500, 500, 0, 200),
                                            (250, 270, 0, 400)])
 def test_deep_parity(pkg, oracle, ctx, lt, ln, fixed, n):
-    """Samples deeper than the main kernel's 256 -> deep kernel (LDS sort);
-    > 255 reads per class saturates w, > 255 total rescales c (Appendix A.4)."""
+    """Sites beyond the main kernel's 512 sort slots -> wide kernel (and the
+    deep kernel past 2048); > 255 reads per class saturates w, > 255 total
+    rescales c (Appendix A.4)."""
     batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=fixed, **EXOTIC), 0, n)
     assert_parity(pkg, oracle, batch, ctx=ctx)
 
 
 def test_kernel_routing_mix(pkg, oracle, ctx):
     """One batch whose sites take every route: main kernel (<= 512 sort slots),
-    wide kernel (<= 2048), deep kernel via the wide kernel's overflow list
-    (<= 4096 per sample), and the giant kernel, interleaved so each kernel sees
+    wide kernel (<= 2048), and the deep kernel via the wide kernel's overflow
+    list (histogram fold, any depth), interleaved so each kernel sees
     non-contiguous site indices."""
     parts = [pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=1, **EXOTIC), 7 * k, n)
              for k, (lt, ln, n) in enumerate([(60, 30, 40), (600, 500, 12), (1500, 1200, 6), (4200, 300, 3),
@@ -104,32 +105,94 @@ def test_pinned_host_batch(pkg, oracle, ctx):
     assert_parity(pkg, oracle, p, ctx=ctx)
 
 
-def test_malformed_offsets_reported(pkg, oracle, ctx):
-    """Decreasing read offsets (a malformed batch) wrap a site's read count to
-    ~2^32.  No kernel may read reads for such a site: it is routed through the
-    deep lists to the giant kernel, which scores it -2 without touching its
-    reads, and ss_ctx_check reports SS_E_INVAL.  Cases: a tumor count of -1
-    (odd: count + pad wraps to a small slot total, the main kernel's trap) and
-    a normal count of -7 next to a wide site.  The context stays usable."""
+def _malformed_base(pkg):
     b = pkg.synth_batch_host(pkg.Synth.default(60, 30, **EXOTIC), 11, 300)
     wide = pkg.synth_batch_host(pkg.Synth.default(700, 600, fixed_depth=1, **EXOTIC), 3, 4)
     sites = [b.site(i) for i in range(b.n_sites)]
     sites[200:200] = [wide.site(i) for i in range(wide.n_sites)]
-    good = pkg.Batch.from_sites(sites)
+    return pkg.Batch.from_sites(sites)
+
+
+def _score_device(pkg, ctx, b):
+    """Score a host batch through ss_score_batch_device; returns (score, rc of ss_ctx_check)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(dev)
+    score = torch.full((b.n_sites,), 12345, dtype=torch.int32, device=dev)
+    ctx.score_device(t(b.ref, np.uint8), t(b.off_tumor, np.int32), t(b.off_normal, np.int32),
+                     t(b.reads_tumor, np.int32), t(b.reads_normal, np.int32), score=score)
+    try:
+        ctx.check()
+        rc = pkg.SS_OK
+    except pkg.SniperError as e:
+        rc = e.code
+    return score.cpu().numpy(), rc
+
+
+@pytest.mark.parametrize("case", ["tumor_minus_1", "normal_minus_7_wide", "past_end", "both_past_end"])
+def test_malformed_offsets_reported(pkg, oracle, ctx, case):
+    """Malformed offsets never steer a load outside the batch's reads, and the
+    batch is reported: ss_ctx_check returns SS_E_INVAL.  A site whose own
+    offsets decrease wraps its read count to ~2^32 and is routed through the
+    deep lists to the deep kernel, which scores it -2 without touching reads.
+    Cases, one malformation per batch: a tumor count of -1 (odd: count + pad
+    wraps to a small slot total, the main kernel's trap), a normal count of -7
+    next to a wide site, an offset past off[n] (so a later site decreases),
+    and two offsets past the end with equal values (a zero-length site between
+    them, then the decrease).  The context stays usable."""
+    good = _malformed_base(pkg)
     ot, on = good.off_tumor.copy(), good.off_normal.copy()
-    assert ot[5] >= 1 and on[202] >= 7
-    ot[6] = ot[5] - 1
-    on[203] = on[202] - 7
+    n = good.n_sites
+    if case == "tumor_minus_1":
+        assert ot[5] >= 1
+        ot[6] = ot[5] - 1
+        minus2 = [5]
+    elif case == "normal_minus_7_wide":
+        assert on[202] >= 7
+        on[203] = on[202] - 7
+        minus2 = [202]
+    elif case == "past_end":
+        ot[100] = ot[n] + 1000                        # site 99 runs past the end, site 100 decreases
+        minus2 = [100]
+    else:
+        ot[50] = ot[51] = ot[n] + 77
+        minus2 = [51]
     bad = pkg.Batch(good.ref, ot, on, good.reads_tumor, good.reads_normal)
     with pytest.raises(pkg.SniperError) as ei:
         ctx.score_batch(bad)
     assert ei.value.code == pkg.SS_E_INVAL
     ctx.check()                                   # the sticky bit was cleared
+    score, rc = _score_device(pkg, ctx, bad)
+    assert rc == pkg.SS_E_INVAL
+    assert all(score[i] == -2 for i in minus2), [(i, score[i]) for i in minus2]
+    ref_score, _, _ = ctx.score_batch(good)
+    untouched = [i for i in range(n) if ot[i] == good.off_tumor[i] and ot[i + 1] == good.off_tumor[i + 1]
+                 and on[i] == good.off_normal[i] and on[i + 1] == good.off_normal[i + 1]]
+    assert (score[untouched] == ref_score[untouched]).all()
     assert_parity(pkg, oracle, good, ctx=ctx)
 
 
+def test_deep_kernel_any_depth(pkg, oracle, ctx):
+    """The deep kernel has no depth limit: one site with 1.1 M tumor reads and
+    ~10^5 normal reads (the round-1 build gave up beyond 2^20 per sample) next
+    to ordinary sites, bit-exact with the oracle."""
+    big = pkg.synth_batch_host(pkg.Synth.default(1_100_000, 100_000, fixed_depth=1, **EXOTIC), 0, 1)
+    small = pkg.synth_batch_host(pkg.Synth.default(60, 30, **EXOTIC), 9, 50)
+    sites = [small.site(i) for i in range(25)] + [big.site(0)] + [small.site(i) for i in range(25, 50)]
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), ctx=ctx)
+    ctx.check()
+
+
+def test_many_deep_sites(pkg, oracle, ctx):
+    """Thousands of sites beyond the wide kernel's 2048 slots in one batch:
+    the deep list is sized from the batch (no fixed cap, no overflow)."""
+    b = pkg.synth_batch_host(pkg.Synth.default(1200, 1000, **EXOTIC), 0, 3000)
+    assert_parity(pkg, oracle, b, ctx=ctx)
+    ctx.check()
+
+
 def test_giant_parity(pkg, oracle, ctx):
-    """> 4096 reads in a sample -> giant kernel with global scratch."""
+    """> 4096 reads in a sample (the round-1 giant route) -> deep kernel."""
     big = pkg.synth_batch_host(pkg.Synth.default(6000, 4500, fixed_depth=1, **EXOTIC), 0, 6)
     small = pkg.synth_batch_host(pkg.Synth.default(40, 40, **EXOTIC), 100, 20)
     sites = [big.site(i) for i in range(big.n_sites)] + [small.site(i) for i in range(small.n_sites)]
@@ -174,6 +237,12 @@ def quirk_sites(pkg):
     for n in (63, 64, 65, 127, 128, 129, 255, 256, 257):
         s.append(("C", [R(60, 10 + (i * 7) % 31, C_ if i % 9 else G, i & 1) for i in range(n)],
                   [R(60, 10 + (i * 5) % 31, C_, (i >> 1) & 1) for i in range(n // 2 + 1)]))
+    # every key field at its maximum in the NORMAL sample (mapQ = baseQ = 255,
+    # T, reverse strand): a contributing read whose 16-bit sort key would equal
+    # the pad key; at main-kernel, wide-kernel and deep-kernel depths
+    for nt_, nn_ in ((10, 10), (300, 300), (1500, 1000)):
+        s.append(("A", [R(60, 30, A)] * nt_,
+                  [R(255, 255, T, 1)] * (nn_ // 2) + [R(255, 255, T, i & 1) for i in range(nn_ - nn_ // 2)]))
     return s
 
 

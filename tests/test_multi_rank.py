@@ -2,7 +2,9 @@
 rank scores only its own region with no data-path collective, the per-rank
 results are exactly the corresponding slices of a single-process run, and the
 bench aggregation takes the max time and the summed sites over ranks.
-The scorer here is the CPU oracle (the GPU path is covered by -m gpu tests)."""
+The CPU tests score with the oracle; the -m gpu tests run the same sharding
+on the HIP path (one context per rank) and several contexts / streams in one
+process."""
 import os
 import socket
 
@@ -79,3 +81,117 @@ def test_shard_contigs_partition():
         assert max(loads) <= sum(lengths) / world + max(lengths)
         assert all(p == sorted(p) for p in plan)
     assert sh.shard_range(10, 3, 0) == (0, 4) and sh.shard_range(10, 3, 2) == (7, 10)
+
+
+# ------------------------------------------------------------------ GPU ranks
+def _gpu_worker(rank, world, port, out_dir):
+    """One rank of a region-sharded run on the HIP path: its own context on
+    cuda:(rank % devices), its own shard, no data-path collective."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from __graft_entry__ import load_package
+    import importlib
+    pkg = load_package()
+    sharding = importlib.import_module("somatic_sniper_amd.sharding")
+    dev = rank % torch.cuda.device_count()
+    n = 20000
+    first, last = sharding.shard_range(n, world, rank)
+    b = pkg.synth_batch_host(pkg.Synth.default(60, 30, p_somatic=0.02, p_germline=0.02), first, last - first)
+    with pkg.Context(pkg.Params.default(), device=dev) as ctx:
+        score, calls, glf = ctx.score_batch(b, want_glf=True)
+    calls = calls.copy()
+    calls["site"] += first                       # shard-local -> global site index
+    np.save(os.path.join(out_dir, f"score{rank}.npy"), score)
+    np.save(os.path.join(out_dir, f"glf{rank}.npy"), glf.view(np.uint8))
+    np.save(os.path.join(out_dir, f"calls{rank}.npy"), calls.view(np.uint8))
+    np.save(os.path.join(out_dir, f"dev{rank}.npy"), np.array([dev]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_ranks_equal_single_context(tmp_path, pkg, world):
+    """world gloo ranks, each scoring its contiguous shard on its own HIP
+    context (ranks share the box's GPU when it has fewer), concatenate to a
+    single-context run of the whole range: scores, glf records and calls."""
+    mp.spawn(_gpu_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    b = pkg.synth_batch_host(pkg.Synth.default(60, 30, p_somatic=0.02, p_germline=0.02), 0, 20000)
+    with pkg.Context(pkg.Params.default(), device=0) as ctx:
+        full, fcalls, fglf = ctx.score_batch(b, want_glf=True)
+    parts = np.concatenate([np.load(tmp_path / f"score{r}.npy") for r in range(world)])
+    assert (parts == full).all()
+    g = np.concatenate([np.load(tmp_path / f"glf{r}.npy") for r in range(world)])
+    assert (g == fglf.view(np.uint8)).all()
+    c = np.concatenate([np.load(tmp_path / f"calls{r}.npy") for r in range(world)])
+    assert len(fcalls) > 0 and (c.reshape(-1) == fcalls.view(np.uint8).reshape(-1)).all()
+    import torch
+    ndev = torch.cuda.device_count()
+    assert [int(np.load(tmp_path / f"dev{r}.npy")[0]) for r in range(world)] == [r % ndev for r in range(world)]
+
+
+@pytest.mark.gpu
+def test_two_contexts_interleaved(pkg):
+    """Two contexts in one process (on two devices when the box has them, else
+    both on cuda:0), with different parameters, scoring interleaved batches of
+    different shapes: per-context work lists and counters stay separate."""
+    import torch
+    from oracle import binding as ob
+    ndev = torch.cuda.device_count()
+    ca = pkg.Context(pkg.Params.default(), device=0)
+    cb = pkg.Context(pkg.Params.default(use_joint_priors=1), device=1 % ndev)
+    try:
+        ba = [pkg.synth_batch_host(pkg.Synth.default(60, 30, p_somatic=0.03), 100 * k, 4000) for k in range(3)]
+        bb = [pkg.synth_batch_host(pkg.Synth.default(500, 400, p_somatic=0.03), 7 * k, 300) for k in range(3)]
+        got = []
+        for x, y in zip(ba, bb):
+            got.append((ca.score_batch(x)[0], cb.score_batch(y)[0]))
+        oa, ojb = ob.Oracle(), ob.Oracle(ob.opts_to_params(["-J"]))
+        for (sa, sb), x, y in zip(got, ba, bb):
+            assert (sa == oa.score_batch(x.ref, x.off_tumor, x.off_normal, x.reads_tumor, x.reads_normal,
+                                         want_glf=False)[0]).all()
+            assert (sb == ojb.score_batch(y.ref, y.off_tumor, y.off_normal, y.reads_tumor, y.reads_normal,
+                                          want_glf=False)[0]).all()
+        ca.check()
+        cb.check()
+    finally:
+        ca.close()
+        cb.close()
+
+
+@pytest.mark.gpu
+def test_one_context_two_streams(pkg):
+    """ss_score_batch_device on two streams of one context back to back: the
+    second launch waits for the first (shared work lists), so both batches are
+    scored as if alone."""
+    import torch
+    dev = torch.device("cuda", 0)
+    ctx = pkg.Context(pkg.Params.default(), device=0)
+    try:
+        syn = pkg.Synth.default(500, 500, p_somatic=0.02)
+        d1 = ctx.synth_device(syn, 0, 20000, device=dev)
+        d2 = ctx.synth_device(pkg.Synth.default(60, 30, p_somatic=0.02), 0, 200000, device=dev)
+        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        o1 = torch.empty(20000, dtype=torch.int32, device=dev)
+        o2 = torch.empty(200000, dtype=torch.int32, device=dev)
+        for _ in range(3):
+            ctx.score_device(d1["ref"], d1["off_tumor"], d1["off_normal"], d1["reads_tumor"], d1["reads_normal"],
+                             score=o1, stream=s1)
+            ctx.score_device(d2["ref"], d2["off_tumor"], d2["off_normal"], d2["reads_tumor"], d2["reads_normal"],
+                             score=o2, stream=s2)
+        torch.cuda.synchronize(dev)
+        ctx.check()
+        r1 = torch.empty_like(o1)
+        r2 = torch.empty_like(o2)
+        ctx.score_device(d1["ref"], d1["off_tumor"], d1["off_normal"], d1["reads_tumor"], d1["reads_normal"], score=r1)
+        torch.cuda.synchronize(dev)
+        ctx.score_device(d2["ref"], d2["off_tumor"], d2["off_normal"], d2["reads_tumor"], d2["reads_normal"], score=r2)
+        torch.cuda.synchronize(dev)
+        assert torch.equal(o1, r1) and torch.equal(o2, r2)
+    finally:
+        ctx.close()
