@@ -170,6 +170,77 @@ def host_cores():
         return os.cpu_count() or 1, "os.cpu_count"
 
 
+# PMC passes bench.py runs on itself (rank 0, N=1): one rocprofv3 process per
+# pass (counters of different blocks / slot budgets never share a pass).
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
+              ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+               "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"))
+
+
+def pmc_child(args):
+    """--pmc-child: the bench's batch 0 of shard 0 scored a few times, nothing
+    else (run under rocprofv3 by live_counters)."""
+    import torch
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    dev = torch.device("cuda", 0)
+    ctx = pkg.Context(pkg.Params.default(), device=0)
+    d = ctx.synth_device(pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=0), 0, args.sites, device=dev)
+    score = torch.empty(args.sites, dtype=torch.int32, device=dev)
+    for _ in range(args.pmc_launches):
+        ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"], score=score)
+    torch.cuda.synchronize(dev)
+    ctx.check()
+    ctx.close()
+
+
+def live_counters(args, kernel="ss_score_main"):
+    """rocprofv3 --pmc passes over a child that scores the bench's own batch
+    (same sites, depths, seed): per-launch means of `kernel`'s counters, the
+    first launch dropped (cold tables).  None when rocprofv3 is missing or a
+    pass fails -- the timed result never depends on it."""
+    import csv
+    import re
+    import shutil
+    import tempfile
+    exe = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if exe is None:
+        return None
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    env["TMPDIR"] = "/tmp"
+    vals = {}
+    for counters in PMC_PASSES:
+        out = tempfile.mkdtemp(prefix="ss_pmc_", dir="/tmp")
+        try:
+            cmd = [exe, "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "run", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-child", "--sites", str(args.sites),
+                   "--lt", str(args.lt), "--ln", str(args.ln), "--seed", str(args.seed),
+                   "--pmc-launches", str(args.pmc_launches)]
+            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
+            path = None
+            for dp, _, fs in os.walk(out):
+                if "run_counter_collection.csv" in fs:
+                    path = os.path.join(dp, "run_counter_collection.csv")
+            if r.returncode != 0 or path is None:
+                print(f"bench: PMC pass {counters} failed (rc {r.returncode}): {r.stderr[-500:]}", file=sys.stderr)
+                return None
+            per = {}
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    if re.search(re.escape(kernel) + r"[<(]", row["Kernel_Name"]):
+                        d = per.setdefault(int(row["Dispatch_Id"]), {})
+                        d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+            ds = sorted(per)[1:] or sorted(per)
+            for c in counters:
+                vals[c] = float(np.mean([per[k].get(c, 0.0) for k in ds]))
+        except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
+            print(f"bench: PMC pass {counters} failed: {e}", file=sys.stderr)
+            return None
+        finally:
+            shutil.rmtree(out, ignore_errors=True)
+    return vals
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -195,8 +266,12 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL; gloo rehearses N ranks on one GPU)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 counter passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-launches", type=int, default=3, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.pmc_child:
+        return pmc_child(args)
 
     bad = [k for k in REFUSED_ENV if os.environ.get(k)]
     if bad:
@@ -306,15 +381,6 @@ def main():
     avg_kernel_ms = float(np.mean(kms)) if len(kms) else None
     alg_bytes = float(np.mean([bytes_per_batch[k] for k in used]))
     achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms else None
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if dom == "main" and tj.get("sites") == S and tj.get("lt") == args.lt and tj.get("ln") == args.ln:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
     result = {
         "metric": METRIC,
         "value": round(total_sites / elapsed, 1),
@@ -341,12 +407,37 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-            "traffic": traffic,
+            "traffic": None,
             "algorithmic_bytes_per_launch": alg_bytes,
             "avg_kernel_ms": round(avg_kernel_ms, 4) if avg_kernel_ms else None,
             "avg_ms_by_kernel": {k: round(v, 4) for k, v in kmean.items()},
         },
     }
+    if rank == 0 and world == 1 and not args.no_pmc:
+        # live counters of the dominant kernel on this same workload (separate
+        # rocprofv3 passes after the timed region; MI355X_MICROARCH.md: FETCH_SIZE
+        # reports half the streamed read bytes on gfx950 and is doubled, both KiB;
+        # SQ_* wave counters, GRBM_GUI_ACTIVE = busy cycles summed over 8 XCDs)
+        pc = live_counters(args, result["roofline"]["kernel"])
+        if pc:
+            rd, wr = 2.0 * pc["FETCH_SIZE"] * 1024.0, pc["WRITE_SIZE"] * 1024.0
+            rf = result["roofline"]
+            rf["traffic"] = rd + wr
+            rf["traffic_over_algorithmic"] = round((rd + wr) / alg_bytes, 4)
+            cyc = pc["GRBM_GUI_ACTIVE"] / 8.0                       # kernel cycles
+            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+            rf["valu"] = {
+                "insts_per_site": round(pc["SQ_INSTS_VALU"] / S, 1),
+                "salu_per_site": round(pc["SQ_INSTS_SALU"] / S, 1),
+                "lds_per_site": round(pc["SQ_INSTS_LDS"] / S, 1),
+                # VALU issue fraction: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+                "issue_frac": round(2.0 * pc["SQ_INSTS_VALU"] / (cyc * simds), 4) if cyc else None,
+                "wave_cycles_split": {k: round(pc[c] / pc["SQ_WAVE_CYCLES"], 3) for k, c in
+                                      (("issue", "SQ_ACTIVE_INST_ANY"), ("issue_stall", "SQ_WAIT_INST_ANY"),
+                                       ("waitcnt", "SQ_WAIT_ANY"))} if pc["SQ_WAVE_CYCLES"] else None,
+                "clock_ghz_est": round(cyc / (avg_kernel_ms * 1e-3) / 1e9, 3) if avg_kernel_ms else None,
+                "source": "rocprofv3 --pmc, separate passes, same batch, mean of launches 2..",
+            }
     if rank == 0 and world == 1 and not args.no_cpu:
         pre = score[0][: args.cpu_sample].cpu().numpy() if S >= args.cpu_sample else None
         result["cpu_baseline"] = cpu_baseline(args.lt, args.ln, min(args.cpu_sample, S), args.seed, pre)

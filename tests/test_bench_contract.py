@@ -23,6 +23,12 @@ def test_bench_json_contract():
     rf = r["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    import shutil
+    if shutil.which("rocprofv3") or os.path.exists("/opt/rocm/bin/rocprofv3"):
+        # live PMC passes: HBM traffic of the timed kernel and its VALU issue share
+        assert rf["traffic"] and 0.5 < rf["traffic_over_algorithmic"] < 3.0, rf
+        v = rf["valu"]
+        assert v["insts_per_site"] > 50 and 0 < v["issue_frac"] < 1.0, v
     cb = r["cpu_baseline"]
     assert cb["cores"] == 1 and cb["value"] > 0 and cb["parity_vs_gpu"] is True
 
