@@ -44,8 +44,9 @@ void ss_dqstats_packed(const uint32_t *r, uint32_t n, int ref_base4, uint32_t wa
     if (q->total_depth) q->total_mean_mapQ = (uint32_t)(q->total_mean_mapQ / (double)q->total_depth + .499);
 }
 
-/* comma list of values[i] for the bases in `bases`, "0" when none */
-static void put_masked(FILE *fh, int bases, const uint32_t v[4])
+/* comma list of values[i] for the bases in `bases`, "0" when none
+ * (print_mean_quality_values / print_base_count, dqstats.c:55-87) */
+void ss_put_masked(FILE *fh, int bases, const uint32_t v[4])
 {
     int any = 0;
     for (int i = 0; i < 4; ++i)
@@ -68,17 +69,17 @@ static void write_classic(FILE *fh, const ss_site_out_t *s)
     for (int k = 0; k < 2; ++k) {
         const ss_sample_out_t *x = smp[k];
         const int alt = ~s->ref_base4 & x->genotype;
-        put_masked(fh, s->ref_base4, x->dq.mean_baseQ);
+        ss_put_masked(fh, s->ref_base4, x->dq.mean_baseQ);
         fputc('\t', fh);
-        put_masked(fh, s->ref_base4, x->dq.mean_mapQ);
+        ss_put_masked(fh, s->ref_base4, x->dq.mean_mapQ);
         fputc('\t', fh);
-        put_masked(fh, s->ref_base4, x->dq.base_occ);
+        ss_put_masked(fh, s->ref_base4, x->dq.base_occ);
         fputc('\t', fh);
-        put_masked(fh, alt, x->dq.mean_baseQ);
+        ss_put_masked(fh, alt, x->dq.mean_baseQ);
         fputc('\t', fh);
-        put_masked(fh, alt, x->dq.mean_mapQ);
+        ss_put_masked(fh, alt, x->dq.mean_mapQ);
         fputc('\t', fh);
-        put_masked(fh, alt, x->dq.base_occ);
+        ss_put_masked(fh, alt, x->dq.base_occ);
         fputc(k == 0 ? '\t' : '\n', fh);
     }
 }

@@ -34,6 +34,8 @@ const char *ss_format_name(int i);
 int  ss_format_count(void);
 void ss_write_header(FILE *fh, int fmt, const char *refseq, const char *normal_id, const char *tumor_id);
 void ss_write_site(FILE *fh, int fmt, const ss_site_out_t *s);
+/* print_mean_quality_values / print_base_count (dqstats.c:55-87) */
+void ss_put_masked(FILE *fh, int bases, const uint32_t values[4]);
 void ss_dqstats_packed(const uint32_t *reads, uint32_t n, int ref_base4, uint32_t wanted, ss_dqstats_t *q);
 
 #endif

@@ -143,3 +143,47 @@ def test_native_cli_matches_reference(datasets, fmt):
             assert strip(nat) == strip(ref), (d, fmt, opts)
             quiet = lambda e: e.replace("[fai_load] build FASTA index.\n", "")
             assert quiet(pn.stderr) == quiet(pr.stderr), (pn.stderr, pr.stderr)
+
+
+@need_native
+@need_ref
+def test_bad_output_format_matches_reference(datasets, tmp_path):
+    """-F with an unknown name (output_format.c:31-32): same message, exit code
+    and (empty) output file as the reference CLI, before any GPU work."""
+    d, fa, t, n = datasets[0]
+    pr = _run([REF_CLI, "-F", "foo", "-f", fa, t, n, "ref.out"], d)
+    pn = _run([NATIVE, "-F", "foo", "-f", fa, t, n, "nat.out"], d)
+    quiet = lambda e: e.replace("[fai_load] build FASTA index.\n", "")
+    assert pr.returncode == pn.returncode == 1
+    assert quiet(pn.stderr) == quiet(pr.stderr) and "unknown output format: 'foo'. Abort!" in pn.stderr
+    assert open(os.path.join(d, "nat.out")).read() == open(os.path.join(d, "ref.out")).read()
+
+
+@pytest.mark.gpu
+@need_native
+@need_ref
+@pytest.mark.parametrize("fmt", ["vcf", "classic"])
+def test_sample_ids_and_stdin_match_reference(datasets, fmt):
+    """-n / -t sample names in the VCF header (output_vcf.c:189-191) and the
+    tumor BAM read from stdin as '-' (main.c:128), byte-identical to the
+    reference CLI given the same arguments."""
+    strip = lambda s: "".join(l for l in s.splitlines(True) if not l.startswith("##fileDate"))
+    for d, fa, t, n in datasets[:3]:
+        args = ["-F", fmt, "-n", "NORMAL_X", "-t", "TUMOR_Y", "-f", fa]
+        pr = _run([REF_CLI] + args + [t, n, "ref_ids.out"], d)
+        pn = _run([NATIVE] + args + [t, n, "nat_ids.out"], d)
+        assert pr.returncode == 0 and pn.returncode == 0, (pr.stderr, pn.stderr)
+        ref = open(os.path.join(d, "ref_ids.out")).read()
+        assert strip(open(os.path.join(d, "nat_ids.out")).read()) == strip(ref)
+        if fmt == "vcf":
+            assert "NORMAL_X\tTUMOR_Y" in ref
+        outs = []
+        for cli, name in ((REF_CLI, "ref_stdin.out"), (NATIVE, "nat_stdin.out")):
+            with open(os.path.join(d, t), "rb") as fin:
+                p = subprocess.run([cli, "-F", fmt, "-f", fa, "-", n, name], cwd=d, stdin=fin,
+                                   capture_output=True, text=True, timeout=600)
+            assert p.returncode == 0, p.stderr
+            outs.append((strip(open(os.path.join(d, name)).read()), p.stderr))
+        assert outs[0][0] == outs[1][0]
+        quiet = lambda e: e.replace("[fai_load] build FASTA index.\n", "")
+        assert quiet(outs[0][1]) == quiet(outs[1][1])
