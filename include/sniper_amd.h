@@ -204,6 +204,16 @@ int  ss_table_hashes(const ss_ctx_t *ctx, uint64_t *fk, uint64_t *coef,
  * ss_model_check / ss_ctx_create fail with SS_E_TABLES. */
 int  ss_model_check(const ss_params_t *p, uint64_t hashes[3], float *q_r);
 int  ss_model_pinned(const uint64_t hashes[3]);
+/* Where the calling thread's latest table set came from: the fk / coef / lhet
+ * tables (sniper_maqcns.c:27-100, 0.6 s of x87 work) are built once per
+ * process and table parameters, and kept in a disk cache keyed by those
+ * parameters and the machine (SS_TABLE_CACHE=<dir>, default
+ * ~/.cache/sniper_amd; SS_TABLE_CACHE=off disables it).  A cached blob is
+ * verified against its recorded hashes before use.  -1 before any build. */
+#define SS_TABLES_BUILT   0
+#define SS_TABLES_PROCESS 1
+#define SS_TABLES_DISK    2
+int  ss_model_last_source(void);
 /* Copy of the host tables (for tests): any pointer may be NULL. */
 int  ss_table_copy(const ss_ctx_t *ctx, double *fk, double *coef, double *lhet,
                    int *qadd1024, int *prior160, int *jprior1600);

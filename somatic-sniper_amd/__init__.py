@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "ss_score_batch_device", "ss_score_batch_host", "ss_ctx_check", "ss_table_hashes",
     "ss_table_copy", "ss_synth_default", "ss_synth_batch_host", "ss_synth_batch_device",
     "ss_set_kernel_timing", "ss_last_kernel_ms", "ss_kernel_time_log", "ss_kernel_time_log_k", "ss_model_check", "ss_model_pinned",
+    "ss_model_last_source",
     "ss_host_alloc", "ss_host_free",
 )
 
@@ -239,6 +240,7 @@ def load_library():
     lib.ss_last_kernel_ms.restype = C.c_double
     lib.ss_model_check.argtypes = [vp, vp, vp]
     lib.ss_model_pinned.argtypes = [vp]
+    lib.ss_model_last_source.restype = C.c_int
     lib.ss_kernel_time_log.argtypes = [vp, vp, C.c_int]
     lib.ss_kernel_time_log_k.argtypes = [vp, C.c_int, vp, C.c_int]
     if lib.ss_abi_version() != 1:
@@ -266,7 +268,8 @@ def model_check(params: Params | None = None):
     qr = C.c_float()
     _check(lib.ss_model_check(C.byref(p), h, C.byref(qr)), "ss_model_check")
     return {"fk": f"{h[0]:016x}", "coef": f"{h[1]:016x}", "lhet": f"{h[2]:016x}", "q_r": qr.value,
-            "pinned": bool(lib.ss_model_pinned(h))}
+            "pinned": bool(lib.ss_model_pinned(h)),
+            "source": {0: "built", 1: "process", 2: "disk"}.get(lib.ss_model_last_source(), "none")}
 
 
 def synth_batch_host(synth: Synth, first_site: int, n_sites: int) -> Batch:

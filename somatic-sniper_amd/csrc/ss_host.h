@@ -23,6 +23,8 @@ typedef struct ss_host_model {
     int32_t  jprior[16 * 10 * 10];
     uint64_t h_fk, h_coef, h_lhet;
     int      pinned;        /* default tables equal a pinned reference run */
+    int      source;        /* SS_TABLES_BUILT / _PROCESS / _DISK                */
+    void    *shared;        /* the process-wide table entry coef / lhet belong to */
 } ss_host_model_t;
 
 extern unsigned char ss_nt16_table[256];   /* valid after ss_host_model_build */

@@ -78,12 +78,6 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
-/* bam_nt16_nt4_table (sniper_maqcns.c:19): single-base codes -> 0..3, else 4 */
-__device__ __forceinline__ uint32_t nt16_to_nt4(uint32_t b)
-{
-    return (b != 0u && (b & (b - 1u)) == 0u) ? (uint32_t)__builtin_ctz(b) : 4u;
-}
-
 /* Sum over the 64 lanes with DPP row shifts + row broadcasts (no LDS
  * round trip); the total ends in lane 63 and is returned wave-uniform. */
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)

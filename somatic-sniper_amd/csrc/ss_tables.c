@@ -16,11 +16,27 @@
  *
  * Build flags: -ffp-contract=off, no -ffast-math, no -march (x86-64 SSE2 double
  * + x87 long double, like the reference Release build).
+ *
+ * Reuse: the reference rebuilds 32.5 MB of tables in
+ * every process (0.63 s).  Here a built set is kept for the process (every
+ * later context with the same table parameters shares it) and written to a
+ * disk cache keyed by the table parameters AND the machine (CPU vendor /
+ * family / model / stepping, glibc version): the tables are CPU-dependent, so
+ * a blob is only ever reused on the kind of host that built it.  A blob is
+ * verified against the FNV-1a hashes in its header before use; a corrupt or
+ * mismatching blob is ignored and replaced.  SS_TABLE_CACHE=<dir> chooses the
+ * directory (default $XDG_CACHE_HOME/sniper_amd or ~/.cache/sniper_amd),
+ * SS_TABLE_CACHE=off disables the disk cache.
  */
+#include <errno.h>
+#include <gnu/libc-version.h>
 #include <math.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "ss_host.h"
 
@@ -254,41 +270,284 @@ static int params_are_default(const ss_params_t *p)
            p->eta == d.eta;
 }
 
+/* ------------------------------------------------------- table reuse ---- */
+/* the parameters the big tables depend on (fk/coef: theta, eta; lhet/q_r:
+ * n_hap, het_rate); the Phred tables are rebuilt per context (microseconds) */
+typedef struct {
+    float theta, eta, het_rate;
+    int n_hap;
+} tab_key_t;
+
+typedef struct tab_entry {
+    tab_key_t key;
+    double fk[256];
+    double *coef, *lhet;
+    float q_r;
+    int q_r_int;
+    uint64_t h_fk, h_coef, h_lhet;
+    struct tab_entry *next;
+} tab_entry_t;
+
+static pthread_mutex_t g_tab_lock = PTHREAD_MUTEX_INITIALIZER;
+static tab_entry_t *g_tabs;               /* kept for the life of the process */
+static __thread int g_last_source = -1;
+static int g_warned_unpinned;
+
+#define SS_COEF_N ((size_t)64 << 16)
+#define SS_LHET_N ((size_t)65536)
+#define SS_BLOB_MAGIC 0x3130424154535353ull   /* "SSSTAB01" */
+
+typedef struct {
+    uint64_t magic, key_hash;
+    uint64_t h_fk, h_coef, h_lhet;       /* FNV-1a-64 (the pinning hashes) */
+    uint64_t check;                      /* word-wise checksum of the payload (integrity) */
+    float q_r;
+    int32_t q_r_int;
+    uint64_t payload;                      /* bytes after the header */
+} blob_hdr_t;
+
+static tab_key_t tab_key(const ss_params_t *p)
+{
+    tab_key_t k;
+    memset(&k, 0, sizeof k);
+    k.theta = p->theta;
+    k.eta = p->eta;
+    k.het_rate = p->het_rate;
+    k.n_hap = p->n_hap;
+    return k;
+}
+
+/* machine signature: what the tables' last bits depend on */
+static void machine_sig(char *out, size_t cap)
+{
+    char vendor[64] = "?", family[16] = "?", model[16] = "?", stepping[16] = "?", line[512];
+    FILE *f = fopen("/proc/cpuinfo", "r");
+    if (f) {
+        while (fgets(line, sizeof line, f)) {
+            char *v = strchr(line, ':');
+            if (!v) continue;
+            v += 1 + (v[1] == ' ');
+            v[strcspn(v, "\n")] = 0;
+            if (!strncmp(line, "vendor_id", 9)) snprintf(vendor, sizeof vendor, "%s", v);
+            else if (!strncmp(line, "cpu family", 10)) snprintf(family, sizeof family, "%s", v);
+            else if (!strncmp(line, "model\t", 6)) snprintf(model, sizeof model, "%s", v);
+            else if (!strncmp(line, "stepping", 8)) { snprintf(stepping, sizeof stepping, "%s", v); break; }
+        }
+        fclose(f);
+    }
+    snprintf(out, cap, "%s/%s/%s/%s/glibc-%s/ld%zu", vendor, family, model, stepping, gnu_get_libc_version(),
+             sizeof(long double));
+}
+
+static uint64_t key_hash(const tab_key_t *k)
+{
+    char sig[256];
+    uint64_t h;
+    machine_sig(sig, sizeof sig);
+    h = ss_fnv1a64(k, sizeof *k) ^ 0x9e3779b97f4a7c15ull;
+    return h ^ (ss_fnv1a64(sig, strlen(sig)) * 0x100000001b3ull);
+}
+
+/* cache directory; 0 when the disk cache is off */
+static int cache_dir(char *out, size_t cap)
+{
+    const char *e = getenv("SS_TABLE_CACHE"), *x, *home;
+    if (e && (!strcmp(e, "off") || !strcmp(e, "0") || !*e)) return 0;
+    if (e) snprintf(out, cap, "%s", e);
+    else if ((x = getenv("XDG_CACHE_HOME")) && *x) snprintf(out, cap, "%s/sniper_amd", x);
+    else if ((home = getenv("HOME")) && *home) snprintf(out, cap, "%s/.cache/sniper_amd", home);
+    else return 0;
+    return 1;
+}
+
+static int blob_path(const tab_key_t *k, char *out, size_t cap)
+{
+    char dir[3072];
+    if (!cache_dir(dir, sizeof dir)) return 0;
+    snprintf(out, cap, "%s/tables-%016llx.bin", dir, (unsigned long long)key_hash(k));
+    return 1;
+}
+
+/* word-wise multiplicative checksum (a few GB/s): detects any changed,
+ * missing or moved 8-byte word of a blob */
+static uint64_t blob_check(const tab_entry_t *t)
+{
+    uint64_t h = 0x243f6a8885a308d3ull;
+    const double *parts[3] = {t->fk, t->coef, t->lhet};
+    const size_t lens[3] = {256, SS_COEF_N, SS_LHET_N};
+    int j;
+    for (j = 0; j < 3; ++j) {
+        const uint64_t *w = (const uint64_t *)parts[j];
+        size_t i;
+        for (i = 0; i < lens[j]; ++i) h = (h ^ w[i]) * 0x9e3779b97f4a7c15ull + (uint64_t)i;
+    }
+    return h;
+}
+
+static int blob_load(const tab_key_t *k, tab_entry_t *t)
+{
+    char path[4096];
+    blob_hdr_t h;
+    FILE *f;
+    int ok = 0;
+    if (!blob_path(k, path, sizeof path) || !(f = fopen(path, "rb"))) return 0;
+    if (fread(&h, sizeof h, 1, f) == 1 && h.magic == SS_BLOB_MAGIC && h.key_hash == key_hash(k) &&
+        h.payload == sizeof t->fk + (SS_COEF_N + SS_LHET_N) * sizeof(double) &&
+        fread(t->fk, sizeof t->fk, 1, f) == 1 && fread(t->coef, sizeof(double), SS_COEF_N, f) == SS_COEF_N &&
+        fread(t->lhet, sizeof(double), SS_LHET_N, f) == SS_LHET_N) {
+        ok = blob_check(t) == h.check;                   /* corrupt: rebuild */
+        t->h_fk = h.h_fk;
+        t->h_coef = h.h_coef;
+        t->h_lhet = h.h_lhet;
+        t->q_r = h.q_r;
+        t->q_r_int = h.q_r_int;
+    }
+    fclose(f);
+    return ok;
+}
+
+/* write-to-temp + rename, so a concurrent reader sees a whole blob or none */
+static void blob_store(const tab_key_t *k, const tab_entry_t *t)
+{
+    char path[4096], tmp[4200], dir[3072];
+    blob_hdr_t h;
+    FILE *f;
+    if (!cache_dir(dir, sizeof dir) || !blob_path(k, path, sizeof path)) return;
+    {   /* mkdir -p of the directory */
+        char d[3072];
+        size_t i, n = strlen(dir);
+        memcpy(d, dir, n + 1);
+        for (i = 1; i <= n; ++i)
+            if (d[i] == '/' || d[i] == 0) {
+                const char c = d[i];
+                d[i] = 0;
+                if (mkdir(d, 0755) != 0 && errno != EEXIST) return;
+                d[i] = c;
+            }
+    }
+    snprintf(tmp, sizeof tmp, "%s.%d.tmp", path, (int)getpid());
+    if (!(f = fopen(tmp, "wb"))) return;
+    memset(&h, 0, sizeof h);
+    h.magic = SS_BLOB_MAGIC;
+    h.key_hash = key_hash(k);
+    h.h_fk = t->h_fk;
+    h.h_coef = t->h_coef;
+    h.h_lhet = t->h_lhet;
+    h.check = blob_check(t);
+    h.q_r = t->q_r;
+    h.q_r_int = t->q_r_int;
+    h.payload = sizeof t->fk + (SS_COEF_N + SS_LHET_N) * sizeof(double);
+    if (fwrite(&h, sizeof h, 1, f) == 1 && fwrite(t->fk, sizeof t->fk, 1, f) == 1 &&
+        fwrite(t->coef, sizeof(double), SS_COEF_N, f) == SS_COEF_N &&
+        fwrite(t->lhet, sizeof(double), SS_LHET_N, f) == SS_LHET_N && fclose(f) == 0) {
+        if (rename(tmp, path) != 0) unlink(tmp);
+        return;
+    }
+    fclose(f);
+    unlink(tmp);
+}
+
+/* the entry for p's table parameters: this process's, the disk cache's, or
+ * freshly built (then stored).  Called with g_tab_lock held. */
+static int tab_get(const ss_params_t *p, tab_entry_t **out, int *source)
+{
+    const tab_key_t k = tab_key(p);
+    tab_entry_t *t;
+    ss_host_model_t b;
+    int rc;
+    for (t = g_tabs; t; t = t->next)
+        if (!memcmp(&t->key, &k, sizeof k)) { *out = t; *source = SS_TABLES_PROCESS; return SS_OK; }
+    t = (tab_entry_t *)calloc(1, sizeof *t);
+    if (!t) return SS_E_NOMEM;
+    t->key = k;
+    t->coef = (double *)malloc(SS_COEF_N * sizeof(double));
+    t->lhet = (double *)malloc(SS_LHET_N * sizeof(double));
+    if (!t->coef || !t->lhet) { free(t->coef); free(t->lhet); free(t); return SS_E_NOMEM; }
+    if (blob_load(&k, t)) {
+        *source = SS_TABLES_DISK;
+    } else {
+        memset(&b, 0, sizeof b);
+        b.prm = *p;
+        free(t->coef);
+        free(t->lhet);
+        t->coef = t->lhet = NULL;
+        if ((rc = build_coef(&b)) != SS_OK || (rc = build_lhet(&b)) != SS_OK) {
+            free(b.coef); free(b.lhet); free(t);
+            return rc;
+        }
+        memcpy(t->fk, b.fk, sizeof t->fk);
+        t->coef = b.coef;
+        t->lhet = b.lhet;
+        t->q_r = b.q_r;
+        t->q_r_int = b.q_r_int;
+        t->h_fk = ss_fnv1a64(t->fk, sizeof t->fk);
+        t->h_coef = ss_fnv1a64(t->coef, SS_COEF_N * sizeof(double));
+        t->h_lhet = ss_fnv1a64(t->lhet, SS_LHET_N * sizeof(double));
+        blob_store(&k, t);
+        *source = SS_TABLES_BUILT;
+    }
+    t->next = g_tabs;
+    g_tabs = t;
+    *out = t;
+    return SS_OK;
+}
+
 int ss_host_model_build(const ss_params_t *p, ss_host_model_t *m)
 {
-    int rc;
+    int rc, source = SS_TABLES_BUILT;
+    tab_entry_t *t = NULL;
     memset(m, 0, sizeof(*m));
     if (!p || p->n_hap < 2 || p->n_hap > 255 || !(p->theta > 0.0f) || p->cap_mapQ < 0)
         return SS_E_INVAL;
+    pthread_mutex_lock(&g_tab_lock);
     nt16_table_init();
+    rc = tab_get(p, &t, &source);
+    pthread_mutex_unlock(&g_tab_lock);
+    if (rc != SS_OK) return rc;
     m->prm = *p;
-    if ((rc = build_coef(m)) != SS_OK) goto fail;
-    if ((rc = build_lhet(m)) != SS_OK) goto fail;
+    memcpy(m->fk, t->fk, sizeof m->fk);
+    m->coef = t->coef;                     /* shared, owned by the process-wide entry */
+    m->lhet = t->lhet;
+    m->q_r = t->q_r;
+    m->q_r_int = t->q_r_int;
+    m->h_fk = t->h_fk;
+    m->h_coef = t->h_coef;
+    m->h_lhet = t->h_lhet;
+    m->shared = t;
+    m->source = source;
+    g_last_source = source;
     build_phred(m);
-    m->h_fk = ss_fnv1a64(m->fk, sizeof(m->fk));
-    m->h_coef = ss_fnv1a64(m->coef, ((size_t)64 << 16) * sizeof(double));
-    m->h_lhet = ss_fnv1a64(m->lhet, 65536 * sizeof(double));
     if (params_are_default(p)) {
         const uint64_t h[3] = {m->h_fk, m->h_coef, m->h_lhet};
         const char *strict = getenv("SS_STRICT_TABLES");
         m->pinned = ss_model_pinned(h);
-        if (!m->pinned && strict && strict[0] == '1') {
-            rc = SS_E_TABLES;   /* no pinned reference run produced these tables */
-            goto fail;
+        if (!m->pinned) {
+            if (strict && strict[0] == '1') {
+                memset(m, 0, sizeof(*m));
+                return SS_E_TABLES;   /* no pinned reference run produced these tables */
+            }
+            pthread_mutex_lock(&g_tab_lock);
+            if (!g_warned_unpinned) {
+                g_warned_unpinned = 1;
+                fprintf(stderr, "[sniper_amd] warning: the model tables built on this host (fk %016llx coef %016llx "
+                        "lhet %016llx) match no pinned run of the reference; scores equal the reference's only if "
+                        "it builds the same tables here (SS_STRICT_TABLES=1 refuses such tables)\n",
+                        (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2]);
+            }
+            pthread_mutex_unlock(&g_tab_lock);
         }
     }
     return SS_OK;
-fail:
-    ss_host_model_free(m);
-    return rc;
 }
 
 void ss_host_model_free(ss_host_model_t *m)
 {
-    free(m->coef);
-    free(m->lhet);
+    /* coef / lhet belong to the process-wide entry (reused by later contexts) */
     m->coef = m->lhet = NULL;
+    m->shared = NULL;
 }
+
+int ss_model_last_source(void) { return g_last_source; }
 
 int ss_model_check(const ss_params_t *p, uint64_t hashes[3], float *q_r)
 {

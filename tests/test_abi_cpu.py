@@ -110,3 +110,56 @@ def test_ctx_create_without_gpu_fails_loudly(pkg):
     with pytest.raises(pkg.SniperError) as e:
         pkg.Context(pkg.Params.default())
     assert e.value.code == pkg.SS_E_NODEV
+
+
+# ----------------------------------------------------------- table reuse (8(f) row 3)
+_CHECK = ("import sys, time, json; sys.path.insert(0, {root!r});"
+          "from __graft_entry__ import load_package; pkg = load_package();"
+          "t0 = time.perf_counter(); a = pkg.model_check(pkg.Params.default({kw}));"
+          "t1 = time.perf_counter(); b = pkg.model_check(pkg.Params.default({kw}));"
+          "print(json.dumps(dict(first=a, second=b, secs=t1 - t0)))")
+
+
+def _model_check_proc(cache, kw=""):
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, SS_TABLE_CACHE=str(cache), SNIPER_AMD_NO_TORCH="1")
+    p = subprocess.run([sys.executable, "-c", _CHECK.format(root=ROOT, kw=kw)], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_table_cache_reuse_and_corruption(tmp_path):
+    """The 32 MB x87 tables are built once per process and once per machine:
+    a second context in the process shares them, a later process loads the
+    verified disk blob instead of rebuilding (timed), a corrupted blob is
+    detected by its hashes and rebuilt, other parameters get their own blob,
+    and SS_TABLE_CACHE=off never touches the disk."""
+    cache = tmp_path / "tabs"
+    r1 = _model_check_proc(cache)
+    assert r1["first"]["source"] == "built" and r1["second"]["source"] == "process"
+    blobs = sorted(cache.iterdir())
+    assert len(blobs) == 1 and blobs[0].stat().st_size > 32 << 20
+    r2 = _model_check_proc(cache)
+    assert r2["first"]["source"] == "disk"
+    for k in ("fk", "coef", "lhet", "q_r", "pinned"):
+        assert r2["first"][k] == r1["first"][k], k
+    assert r2["secs"] < r1["secs"] / 3, (r2["secs"], r1["secs"])
+    # corrupt one coef double: detected, rebuilt, the blob rewritten
+    raw = bytearray(blobs[0].read_bytes())
+    raw[4096 + 1234567] ^= 0x40
+    blobs[0].write_bytes(bytes(raw))
+    r3 = _model_check_proc(cache)
+    assert r3["first"]["source"] == "built" and r3["first"]["coef"] == r1["first"]["coef"]
+    assert _model_check_proc(cache)["first"]["source"] == "disk"
+    # a truncated blob is not trusted either
+    blobs[0].write_bytes(bytes(raw[: len(raw) // 2]))
+    assert _model_check_proc(cache)["first"]["source"] == "built"
+    # other table parameters: their own blob
+    r5 = _model_check_proc(cache, kw="theta=0.9")
+    assert r5["first"]["source"] == "built" and r5["first"]["coef"] != r1["first"]["coef"]
+    assert len(list(cache.iterdir())) == 2
+    off = _model_check_proc("off")
+    assert off["first"]["source"] == "built" and off["first"]["coef"] == r1["first"]["coef"]
