@@ -1023,7 +1023,7 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
 
 /* lanes 0..16: off_t[s..s+16], 17..32: ref[s..s+15], 33..49: off_n[s..s+16],
  * 50, 51: off_t[n_sites], off_n[n_sites] (the batch's read counts) */
-__device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s)
+__device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint32_t s)
 {
     /* The block's bases are wave-uniform (scalar registers); the lane offset is
      * made opaque here so the compiler cannot hoist per-lane 64-bit pointers
@@ -1033,7 +1033,7 @@ __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint64_t s
     asm volatile("" : "+v"(lane));
     const uint32_t *ot = a.off_t + s, *on = a.off_n + s;
     const uint8_t *rf = a.ref + s;
-    const uint64_t rem = a.n_sites - s;               /* > 0 */
+    const uint32_t rem = (uint32_t)a.n_sites - s;     /* > 0 */
     uint32_t v = 0;
     if (lane < 17u) {
         if (lane <= rem) v = ot[lane];
@@ -1101,7 +1101,7 @@ __device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
  * malformed, and no load ever leaves the reads), then every site too deep for
  * the packed sort is handed to the wide kernel: one list push per block. */
 __device__ __forceinline__ void begin_block(const ss_score_args &a, uint32_t &desc, uint32_t nsite,
-                                            uint64_t sblk, uint32_t *seg, uint32_t &ndeep)
+                                            uint32_t sblk, uint32_t *seg, uint32_t &ndeep)
 {
     const uint32_t lane = lane_id();
     {
@@ -1121,7 +1121,7 @@ __device__ __forceinline__ void begin_block(const ss_score_args &a, uint32_t &de
     if (mask == 0) return;
     if (deep) {
         const uint32_t d = ndeep + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-        if (d < a.deep_seg_cap) seg[d] = (uint32_t)(sblk + lane);
+        if (d < a.deep_seg_cap) seg[d] = sblk + lane;
         else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
     }
     ndeep += (uint32_t)__popcll(mask);
@@ -1287,13 +1287,15 @@ void ss_score_main(ss_score_args a)
     Slot3 *slot = L.slot[wv];
     SlotRes *res = L.res[wv];
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
-    const uint64_t nwaves = (uint64_t)gridDim.x * (SS_MAIN_BLOCK / 64);
-    const uint64_t nblocks = (a.n_sites + GB - 1) / GB;
+    /* block bookkeeping in 32-bit scalars (n_sites < 2^32, checked on the host) */
+    const uint32_t nwaves = gridDim.x * (SS_MAIN_BLOCK / 64);
+    const uint32_t n_sites = (uint32_t)a.n_sites;
+    const uint32_t nblocks = (n_sites + GB - 1) / GB;
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
 
-    uint64_t blk = (uint64_t)blockIdx.x * (SS_MAIN_BLOCK / 64) + wv;
+    uint32_t blk = blockIdx.x * (SS_MAIN_BLOCK / 64) + wv;
     /* this wave's segment of the deep list; its length is stored on every exit */
-    const uint32_t gw = (uint32_t)blk;
+    const uint32_t gw = blk;
     uint32_t *seg = a.deep_list + (size_t)gw * a.deep_seg_cap;
     uint32_t ndeep = 0;
     if (blk >= nblocks) {
@@ -1302,8 +1304,8 @@ void ss_score_main(ss_score_args a)
         return;
     }
     uint32_t desc = load_desc(a, blk * GB);
-    uint32_t nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
-    uint64_t nblk = blk + nwaves;
+    uint32_t nsite = min(n_sites - blk * GB, (uint32_t)GB);
+    uint32_t nblk = blk + nwaves;
     uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
     begin_block(a, desc, nsite, blk * GB, seg, ndeep);
     Sub cur = form_sub(desc, nsite, 0);
@@ -1315,7 +1317,7 @@ void ss_score_main(ss_score_args a)
             return;
         }
         desc = ndesc;
-        nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
+        nsite = min(n_sites - blk * GB, (uint32_t)GB);
         nblk = blk + nwaves;
         ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
         begin_block(a, desc, nsite, blk * GB, seg, ndeep);
@@ -1344,7 +1346,7 @@ void ss_score_main(ss_score_args a)
                 S2[m].ref16 = rdesc >> 8;
                 tot[m] = S2[m].nt + (S2[m].nt & 1u) + S2[m].nn;   /* sort slots incl. pad */
                 if (lane == 0 && i + (uint32_t)m < cur.b) {
-                    sites[G + m] = (uint32_t)(blk * GB + j);
+                    sites[G + m] = blk * GB + j;
                     refcs[G + m] = rdesc & 0xffffu;      /* ref char | nt16 << 8 */
                 }
             }
@@ -1375,7 +1377,7 @@ void ss_score_main(ss_score_args a)
             blk = nblk;
             if (blk >= nblocks) break;
             desc = ndesc;
-            nsite = (uint32_t)(a.n_sites - blk * GB < GB ? a.n_sites - blk * GB : GB);
+            nsite = min(n_sites - blk * GB, (uint32_t)GB);
             nblk = blk + nwaves;
             ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
             begin_block(a, desc, nsite, blk * GB, seg, ndeep);
