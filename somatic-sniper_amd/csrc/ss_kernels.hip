@@ -995,14 +995,37 @@ __device__ __forceinline__ void fold_sample(const RecT *rec, const uint32_t cnt[
         const uint32_t s0 = b == 0 ? 0u : (b == 1 ? start1 : (b == 2 ? start2 : start3));
         const uint32_t t = b == 0 ? cnt[0] : (b == 1 ? cnt[1] : (b == 2 ? cnt[2] : cnt[3]));
         const RecT *p0 = rec + s0;
-        const RecT *p = p0 + t;
         float e = 0.0f;
         uint32_t W = 0;
-        SS_UNROLL(SS_FOLD_UNROLL)
-        while (p != p0) {
-            --p;
-            const uint32_t r = *p;
-            const uint32_t sh = RecForm<RecT>::shift(r);  /* 0 or 16 */
+        uint32_t k = t;                               /* records left, walked from the top */
+        /* batches of SS_FOLD_UNROLL: the records and their fk[w] * m terms are
+         * all loaded / formed before the dependent chain, which is then only
+         * (double)e + term -> (float), as in the reference */
+        while (k >= (uint32_t)SS_FOLD_UNROLL) {
+            double term[SS_FOLD_UNROLL];
+            uint32_t w8[SS_FOLD_UNROLL], m[SS_FOLD_UNROLL];
+#pragma unroll
+            for (int j = 0; j < SS_FOLD_UNROLL; ++j) {
+                const uint32_t r = p0[k - 1u - (uint32_t)j];
+                const uint32_t sh = RecForm<RecT>::shift(r);   /* 0 or 16 */
+                const uint32_t w = __builtin_amdgcn_ubfe(W, sh, 16u);
+                w8[j] = w < 2040u ? w : 2040u;
+                W += 8u << sh;
+                m[j] = __builtin_amdgcn_ubfe(r, moff, mwid);
+            }
+#pragma unroll
+            for (int j = 0; j < SS_FOLD_UNROLL; ++j) term[j] = *reinterpret_cast<const double *>(fkb + w8[j]);
+            /* keep the scheduler from pairing each load with its use (it would
+             * wait for every fk load on its own) */
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < SS_FOLD_UNROLL; ++j) e = (float)((double)e + term[j] * (double)m[j]);
+            k -= (uint32_t)SS_FOLD_UNROLL;
+        }
+        while (k) {
+            --k;
+            const uint32_t r = p0[k];
+            const uint32_t sh = RecForm<RecT>::shift(r);
             uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
             w8 = w8 < 2040u ? w8 : 2040u;
             W += 8u << sh;

@@ -14,7 +14,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 NAMES = ["wait reads", "A loop", "next sub", "B fold", "C glf fin", "D decide", "prologue", "A keys",
-         "A network", "A counts", "A records", "C dma", "C geno_p", "-", "-", "-"]
+         "A network", "A counts", "A records", "C dma", "C geno_p", "W sort", "W finish", "W other"]
 
 
 def main():
