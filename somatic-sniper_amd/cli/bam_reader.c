@@ -53,7 +53,10 @@ int bam_record_read(bgzf_reader_t *fp, bam_record_t *b)
     b->n_cigar = (uint16_t)(core[3] & 0xffff);
     b->flag = (uint16_t)(core[3] >> 16);
     b->l_seq = (int32_t)core[4];
-    b->l_data = bs - 32;
+    /* the read name is padded with NULs to a multiple of 4 bytes so that the
+     * CIGAR words after it are aligned (the file's layout does not align them) */
+    const int32_t pad = (4 - (b->l_qname & 3)) & 3;
+    b->l_data = bs - 32 + pad;
     if (b->l_data > b->m_data) {
         int32_t m = b->l_data + 64;
         uint8_t *d = (uint8_t *)realloc(b->data, (size_t)m);
@@ -61,7 +64,11 @@ int bam_record_read(bgzf_reader_t *fp, bam_record_t *b)
         b->data = d;
         b->m_data = m;
     }
-    if (rd(fp, b->data, (size_t)b->l_data)) return -1;
+    if (b->l_qname > bs - 32) return -1;
+    if (rd(fp, b->data, (size_t)b->l_qname)) return -1;
+    memset(b->data + b->l_qname, 0, (size_t)pad);
+    if (rd(fp, b->data + b->l_qname + pad, (size_t)(bs - 32 - b->l_qname))) return -1;
+    b->l_qname += pad;
     if (b->l_seq < 0 || (int64_t)b->l_qname + 4 * (int64_t)b->n_cigar + ((b->l_seq + 1) >> 1) + b->l_seq >
                             b->l_data)
         return -1;

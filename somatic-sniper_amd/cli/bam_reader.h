@@ -28,7 +28,7 @@ typedef struct {
     uint8_t mapq;
     uint16_t flag, n_cigar;
     int32_t l_seq;
-    uint8_t l_qname;
+    uint16_t l_qname;    /* incl. the NUL padding that aligns the CIGAR */
     uint8_t *data;        /* qname | cigar (u32) | seq (4-bit) | qual | aux */
     int32_t l_data, m_data;
 } bam_record_t;

@@ -41,3 +41,35 @@ def ctx(pkg):
     c = pkg.Context(pkg.Params.default(), device=0)
     yield c
     c.close()
+
+
+# ---------------------------------------------------------------- BAM datasets
+# contig names that fai_fetch parses as regions: "chrA:5-60" reads chrA[4,60),
+# "chr,B" is looked up as "chrB", "chrZ:100" is absent (all-N reference)
+NAMES = ["chrA", "chrA:5-60", "chr,B", "chrB", "chrZ:100"]
+ITEST = os.path.join(ROOT, "tests", "golden", "integration")
+
+
+@pytest.fixture(scope="session")
+def datasets(tmp_path_factory):
+    """The reference's integration pair plus synthetic BAM pairs (tests/bamgen.py)
+    with indels, skips, masked flags, odd qualities, IUPAC/N/'=', soft-masked and
+    N reference, region-like contig names, unmapped reads, an empty normal BAM,
+    H/P/=/X operations and unsorted positions."""
+    import shutil
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bamgen
+    out = []
+    d = tmp_path_factory.mktemp("itest")
+    for f in os.listdir(ITEST):
+        shutil.copy(os.path.join(ITEST, f), d)
+    out.append((str(d), "small.fa", "t-small.bam", "n-small.bam"))
+    for seed, kw in [(1, {}), (2, dict(depth_t=60, depth_n=30)), (3, dict(exotic=False, lengths=(5000,))),
+                     (4, dict(lengths=(400, 300, 900, 200, 700), depth_t=15, depth_n=12)),
+                     (5, dict(lengths=(600, 500, 400, 500, 300), names=NAMES, unmapped=True)),
+                     (6, dict(lengths=(700, 300), empty_normal=True)),
+                     (7, dict(lengths=(900, 600, 500, 700), odd_cigars=True, unsorted=True))]:
+        d = tmp_path_factory.mktemp(f"pair{seed}")
+        bamgen.make_pair(str(d), seed=seed, **kw)
+        out.append((str(d), "ref.fa", "tumor.bam", "normal.bam"))
+    return out

@@ -23,9 +23,6 @@ need_native = pytest.mark.skipif(not os.path.exists(NATIVE), reason="native CLI 
 need_ref = pytest.mark.skipif(not os.path.exists(REF_CLI), reason="reference CLI not built")
 need_dump = pytest.mark.skipif(not os.path.exists(REF_DUMP), reason="reference dump CLI not built")
 
-# contig names that fai_fetch parses as regions: "chrA:5-60" reads chrA[4,60),
-# "chr,B" is looked up as "chrB", "chrZ:100" is absent (all-N reference)
-NAMES = ["chrA", "chrA:5-60", "chr,B", "chrB", "chrZ:100"]
 OPTSETS = [[], ["-Q", "0"], ["-J"], ["-J", "-s", "1e-5", "-Q", "5"], ["-p", "-Q", "0"],
            ["-L", "-G", "-Q", "0"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-q", "20", "-Q", "0"]]
 
@@ -33,27 +30,6 @@ OPTSETS = [[], ["-Q", "0"], ["-J"], ["-J", "-s", "1e-5", "-Q", "5"], ["-p", "-Q"
 def _run(cmd, cwd, env=None):
     return subprocess.run(cmd, cwd=cwd, capture_output=True, text=True, timeout=600,
                           env=dict(os.environ, **(env or {})))
-
-
-@pytest.fixture(scope="module")
-def datasets(tmp_path_factory):
-    import sys
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import bamgen
-    out = []
-    d = tmp_path_factory.mktemp("itest")
-    for f in os.listdir(ITEST):
-        shutil.copy(os.path.join(ITEST, f), d)
-    out.append((str(d), "small.fa", "t-small.bam", "n-small.bam"))
-    for seed, kw in [(1, {}), (2, dict(depth_t=60, depth_n=30)), (3, dict(exotic=False, lengths=(5000,))),
-                     (4, dict(lengths=(400, 300, 900, 200, 700), depth_t=15, depth_n=12)),
-                     (5, dict(lengths=(600, 500, 400, 500, 300), names=NAMES, unmapped=True)),
-                     (6, dict(lengths=(700, 300), empty_normal=True)),
-                     (7, dict(lengths=(900, 600, 500, 700), odd_cigars=True, unsorted=True))]:
-        d = tmp_path_factory.mktemp(f"pair{seed}")
-        bamgen.make_pair(str(d), seed=seed, **kw)
-        out.append((str(d), "ref.fa", "tumor.bam", "normal.bam"))
-    return out
 
 
 def _dump(cli, d, fa, t, n, opts, native, threads="1"):
