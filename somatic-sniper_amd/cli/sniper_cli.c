@@ -6,18 +6,28 @@
  * (sniper_pileup.c restated), the per-site scoring is the C ABI
  * (include/sniper_amd.h) on the GPU, fed in batches by this file:
  *
- *   pileup thread                      scoring thread
+ *   pileup thread                      scorer threads (one per GPU)
  *   ----------------------------       -------------------------------------
- *   pack sites into batch k      ->    ss_score_batch_host(batch k)
- *   (while k-1 is being scored)        dqstats + writer for every emitted
- *                                      site, in (tid, pos) order
+ *   pack sites into batch k      ->    ss_score_batch_host(batch k) on the
+ *   (while earlier batches are         thread's own context / device, then,
+ *   being scored)                      in batch order, dqstats + writer for
+ *                                      every emitted site ((tid, pos) order)
+ *
+ * Several GPUs (SS_DEVICES=0,1,...): one streaming dual pileup per run (the
+ * reference's, with its first-read-drop and lockstep rules untouched) hands
+ * consecutive batches to whichever device's scorer is free; outputs are
+ * written strictly in batch order, so the file is identical for any number
+ * of devices ("one streaming pileup per BAM feeding all
+ * GPUs" -- the reference does not require indexed BAMs, so a contig-sharded
+ * pileup could not seek).
  *
  * A site is what glf_somatic (somatic_sniper.c:109) sees: the ref char of
  * the cached contig (fai fetch, :112-117) and the non-deleted, mapped reads of
  * both samples (sniper_maqcns.c:147).  There is no CPU scoring path: without a
  * usable GPU the program stops with an error.
  *
- * Environment: SS_DEVICE (GPU index, default 0), SS_BATCH (sites per batch,
+ * Environment: SS_DEVICE (GPU index, default 0), SS_DEVICES (comma list of GPU
+ * indices, overrides SS_DEVICE), SS_BATCH (sites per batch,
  * default 2^20), SS_BGZF_THREADS (inflate threads per BAM, default 4),
  * SS_PILEUP_THREADS (2, default: column pileup, per sample a reader thread and
  * SS_PILEUP_WORKERS (default 3) window builders;
@@ -89,10 +99,12 @@ static void batch_free(batch_t *b)
 }
 
 /* ---- run state --------------------------------------------------------- */
-/* batch ring: the pileup fills one while up to N_BATCH-1 wait for or are in
- * the scorer, so the pileup runs ahead while the GPU scorer is still being
- * created and never waits for one batch's scoring */
-#define N_BATCH 4
+/* batch ring: the pileup fills one while the others wait for, are in, or
+ * wait to be written by the scorers, so the pileup runs ahead while the GPU
+ * scorers are still being created and never waits for one batch's scoring.
+ * Batch s (a sequence number) lives in slot s % n_bat. */
+#define MAX_DEV 16
+#define MAX_BATCH (MAX_DEV + 3)
 
 typedef struct {
     /* reference */
@@ -101,30 +113,38 @@ typedef struct {
     int cur_tid, cur_len;
     char *cur_ref;
     /* scoring */
-    ss_ctx_t *ctx;
     FILE *out;
     int fmt;
-    batch_t bat[N_BATCH];
-    int fill;                 /* batch being filled by the pileup thread */
-    int n_full;               /* filled batches queued for the scorer: fill-n_full .. fill-1 */
+    batch_t bat[MAX_BATCH];
+    int n_bat;
+    uint64_t seq_fill;        /* batch the pileup is filling (= batches submitted) */
+    uint64_t seq_claim;       /* next submitted batch a scorer takes */
+    uint64_t seq_write;       /* next batch to be written (output order) */
     int quit, failed;
-    pthread_t th;
+    pthread_t th[MAX_DEV];
     pthread_mutex_t mu;
     pthread_cond_t cv;
     FILE *dump;
     int pileup_only;
-    /* GPU scorer creation, done on the scorer thread while the pileup runs */
+    /* GPU scorers, created on their threads while the pileup runs */
     ss_params_t prm;
-    int device;
+    int n_dev, device[MAX_DEV];
+    ss_ctx_t *ctx[MAX_DEV];
 } run_t;
 
-static void emit_batch(run_t *R, batch_t *b)
+typedef struct {
+    run_t *R;
+    int k;                    /* scorer index */
+} scorer_arg_t;
+
+/* score batch b on context ctx; returns the number of emitted calls or -1 */
+static long score_batch(run_t *R, ss_ctx_t *ctx, batch_t *b)
 {
     ss_batch_t in = {b->n, b->ref, b->off_t, b->off_n, b->reads_t, b->reads_n};
     uint32_t ncalls = 0, nclamp = 0;
     for (;;) {
         ss_out_t o = {b->score, b->calls, (uint32_t)b->calls_cap, &ncalls, NULL, &nclamp};
-        const int rc = ss_score_batch_host(R->ctx, &in, &o);
+        const int rc = ss_score_batch_host(ctx, &in, &o);
         if (rc == SS_E_CAPACITY && ncalls > b->calls_cap) {
             b->calls_cap = ncalls;
             b->calls = (ss_call_t *)xrealloc(b->calls, b->calls_cap * sizeof(ss_call_t));
@@ -133,10 +153,15 @@ static void emit_batch(run_t *R, batch_t *b)
         if (rc) {
             fprintf(stderr, "[bam-somaticsniper] GPU scoring failed: %s\n", ss_strerror(rc));
             R->failed = 1;
-            return;
+            return -1;
         }
-        break;
+        return (long)ncalls;
     }
+}
+
+/* dqstats + writer for the emitted calls of a scored batch (in site order) */
+static void write_batch(run_t *R, const batch_t *b, uint32_t ncalls)
+{
     for (uint32_t i = 0; i < ncalls; ++i) {
         const ss_call_t *c = &b->calls[i];
         const uint32_t s = c->site;
@@ -187,43 +212,53 @@ static void stamp(const char *what)
 
 static void *scorer_main(void *arg)
 {
-    run_t *R = (run_t *)arg;
+    run_t *R = ((scorer_arg_t *)arg)->R;
+    const int k = ((scorer_arg_t *)arg)->k;
+    ss_ctx_t *ctx = NULL;
     if (!R->pileup_only) {
-        /* host tables + device upload overlap the BAM decode and pileup */
-        const int rc = ss_ctx_create(&R->prm, R->device, &R->ctx);
+        /* host tables (shared by the process) + device upload overlap the BAM decode and pileup */
+        const int rc = ss_ctx_create(&R->prm, R->device[k], &ctx);
         stamp("scorer ready");
         if (rc) {
             fprintf(stderr, "[bam-somaticsniper] cannot create the GPU scorer: %s\n", ss_strerror(rc));
             exit(1);
         }
+        R->ctx[k] = ctx;
     }
     pthread_mutex_lock(&R->mu);
     for (;;) {
-        while (R->n_full == 0 && !R->quit) pthread_cond_wait(&R->cv, &R->mu);
-        if (R->n_full == 0 && R->quit) break;
-        batch_t *b = &R->bat[(R->fill + N_BATCH - R->n_full) % N_BATCH];   /* oldest queued */
+        while (R->seq_claim == R->seq_fill && !R->quit) pthread_cond_wait(&R->cv, &R->mu);
+        if (R->seq_claim == R->seq_fill) break;            /* quit and nothing left */
+        const uint64_t s = R->seq_claim++;
+        batch_t *b = &R->bat[s % (uint64_t)R->n_bat];
         pthread_mutex_unlock(&R->mu);
-        if (!R->failed) emit_batch(R, b);
+        const long ncalls = R->failed ? -1 : score_batch(R, ctx, b);
         stamp("batch scored");
+        pthread_mutex_lock(&R->mu);
+        while (R->seq_write != s) pthread_cond_wait(&R->cv, &R->mu);   /* output in batch order */
+        pthread_mutex_unlock(&R->mu);
+        if (ncalls > 0) write_batch(R, b, (uint32_t)ncalls);
         b->n = b->nt = b->nn = 0;
         pthread_mutex_lock(&R->mu);
-        --R->n_full;
+        ++R->seq_write;
         pthread_cond_broadcast(&R->cv);
     }
     pthread_mutex_unlock(&R->mu);
     return NULL;
 }
 
-/* queue the filled batch for the scorer (in order); continue in the next free one */
+/* queue the filled batch for the scorers (in order); continue in the next
+ * slot once its previous batch has been written */
 static void submit(run_t *R)
 {
     pthread_mutex_lock(&R->mu);
-    while (R->n_full == N_BATCH - 1) pthread_cond_wait(&R->cv, &R->mu);
-    ++R->n_full;
-    R->fill = (R->fill + 1) % N_BATCH;
+    ++R->seq_fill;
     pthread_cond_broadcast(&R->cv);
+    while (R->seq_fill - R->seq_write >= (uint64_t)R->n_bat) pthread_cond_wait(&R->cv, &R->mu);
     pthread_mutex_unlock(&R->mu);
 }
+
+static batch_t *filling(run_t *R) { return &R->bat[R->seq_fill % (uint64_t)R->n_bat]; }
 
 static void pack(batch_t *b, const uint32_t *pk, int np, int tumor)
 {
@@ -258,7 +293,7 @@ static int on_site(int32_t tid, int32_t pos, int n1, int n2, const uint32_t *pk1
         R->cur_ref = fasta_fetch(R->fai, R->h1->name[tid], &R->cur_len);
         R->cur_tid = tid;
     }
-    batch_t *b = &R->bat[R->fill];
+    batch_t *b = filling(R);
     const size_t s = b->n;
     b->ref[s] = (uint8_t)((R->cur_ref && pos < R->cur_len) ? R->cur_ref[pos] : 'N');
     b->tid[s] = (uint32_t)tid;
@@ -393,31 +428,48 @@ int main(int argc, char *argv[])
     if (dump && *dump) R.dump = fopen(dump, "w");
     const int pileup_only = env_int("SS_PILEUP_ONLY", 0);
     const int cap = env_int("SS_BATCH", 1 << 20);
-    for (int k = 0; k < N_BATCH; ++k) batch_init(&R.bat[k], (size_t)(cap > 0 ? cap : 1 << 20));
+    {   /* scorer devices: SS_DEVICES=0,1,.. or SS_DEVICE */
+        const char *devs = getenv("SS_DEVICES");
+        if (devs && *devs) {
+            for (const char *q = devs; *q && R.n_dev < MAX_DEV;) {
+                R.device[R.n_dev++] = atoi(q);
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
+        }
+        if (R.n_dev == 0) R.device[R.n_dev++] = env_int("SS_DEVICE", 0);
+    }
+    R.n_bat = R.n_dev + 3;
+    for (int k = 0; k < R.n_bat; ++k) batch_init(&R.bat[k], (size_t)(cap > 0 ? cap : 1 << 20));
     pthread_mutex_init(&R.mu, NULL);
     pthread_cond_init(&R.cv, NULL);
     R.pileup_only = pileup_only;
     R.prm = prm;
-    R.device = env_int("SS_DEVICE", 0);
-    pthread_create(&R.th, NULL, scorer_main, &R);      /* creates the GPU scorer first */
+    scorer_arg_t sarg[MAX_DEV];
+    for (int k = 0; k < R.n_dev; ++k) {                 /* each creates its GPU scorer first */
+        sarg[k].R = &R;
+        sarg[k].k = k;
+        pthread_create(&R.th[k], NULL, scorer_main, &sarg[k]);
+    }
     ss_write_header(R.out, fmt, fn_fa, normal_id, tumor_id);
     dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, env_int("SS_PILEUP_THREADS", 2), on_site, &R);
     stamp("pileup done");
-    if (R.bat[R.fill].n) submit(&R);
+    if (filling(&R)->n) submit(&R);
     pthread_mutex_lock(&R.mu);
     R.quit = 1;
     pthread_cond_broadcast(&R.cv);
     pthread_mutex_unlock(&R.mu);
-    pthread_join(R.th, NULL);
+    for (int k = 0; k < R.n_dev; ++k) pthread_join(R.th[k], NULL);
     bgzf_close(fp1);
     bgzf_close(fp2);
     bam_header_free(&h1);
     bam_header_free(&h2);
     fasta_index_free(R.fai);
     free(R.cur_ref);
-    for (int k = 0; k < N_BATCH; ++k) batch_free(&R.bat[k]);
+    for (int k = 0; k < R.n_bat; ++k) batch_free(&R.bat[k]);
     stamp("output written");
-    if (R.ctx) ss_ctx_destroy(R.ctx);
+    for (int k = 0; k < R.n_dev; ++k)
+        if (R.ctx[k]) ss_ctx_destroy(R.ctx[k]);
     if (R.dump) fclose(R.dump);
     fclose(R.out);
     stamp("exit");

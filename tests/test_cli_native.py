@@ -163,3 +163,24 @@ def test_sample_ids_and_stdin_match_reference(datasets, fmt):
         assert outs[0][0] == outs[1][0]
         quiet = lambda e: e.replace("[fai_load] build FASTA index.\n", "")
         assert quiet(outs[0][1]) == quiet(outs[1][1])
+
+
+@pytest.mark.gpu
+@need_native
+@need_ref
+def test_multi_scorer_output_identical(datasets):
+    """SS_DEVICES with several scorers (all on the box's one GPU here; one
+    per device on a multi-GPU node) and small batches, so consecutive batches
+    are scored concurrently by different contexts: the output is written in
+    batch order and equals the single-scorer run and the reference CLI."""
+    for d, fa, t, n in datasets:
+        for fmt in ("classic", "vcf"):
+            args = ["-F", fmt, "-Q", "0", "-f", fa, t, n]
+            pr = _run([REF_CLI] + args + ["ref_ms.out"], d)
+            p1 = _run([NATIVE] + args + ["one_ms.out"], d, {"SS_BATCH": "97"})
+            p3 = _run([NATIVE] + args + ["three_ms.out"], d, {"SS_BATCH": "97", "SS_DEVICES": "0,0,0"})
+            assert pr.returncode == p1.returncode == p3.returncode == 0, (p1.stderr, p3.stderr)
+            strip = lambda s: "".join(l for l in s.splitlines(True) if not l.startswith("##fileDate"))
+            ref = strip(open(os.path.join(d, "ref_ms.out")).read())
+            assert strip(open(os.path.join(d, "one_ms.out")).read()) == ref
+            assert strip(open(os.path.join(d, "three_ms.out")).read()) == ref, (d, fmt)
