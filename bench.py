@@ -216,7 +216,7 @@ def live_counters(args, kernel="ss_score_main"):
                    sys.executable, os.path.abspath(__file__), "--pmc-child", "--sites", str(args.sites),
                    "--lt", str(args.lt), "--ln", str(args.ln), "--seed", str(args.seed),
                    "--pmc-launches", str(args.pmc_launches)]
-            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
+            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
             path = None
             for dp, _, fs in os.walk(out):
                 if "run_counter_collection.csv" in fs:
