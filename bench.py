@@ -216,7 +216,17 @@ def live_counters(args, kernel="ss_score_main"):
                    sys.executable, os.path.abspath(__file__), "--pmc-child", "--sites", str(args.sites),
                    "--lt", str(args.lt), "--ln", str(args.ln), "--seed", str(args.seed),
                    "--pmc-launches", str(args.pmc_launches)]
-            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
+            # own process group: a pass that overruns is killed with its python child
+            proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                    text=True, start_new_session=True)
+            try:
+                _, err = proc.communicate(timeout=150)
+            except subprocess.TimeoutExpired:
+                import signal
+                os.killpg(proc.pid, signal.SIGKILL)
+                proc.communicate()
+                raise
+            r = subprocess.CompletedProcess(cmd, proc.returncode, "", err)
             path = None
             for dp, _, fs in os.walk(out):
                 if "run_counter_collection.csv" in fs:
