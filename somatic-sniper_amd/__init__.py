@@ -240,7 +240,8 @@ def load_library():
     lib.ss_last_kernel_ms.restype = C.c_double
     lib.ss_model_check.argtypes = [vp, vp, vp]
     lib.ss_model_pinned.argtypes = [vp]
-    lib.ss_model_last_source.restype = C.c_int
+    if hasattr(lib, "ss_model_last_source"):      # absent from round-1 builds (A/B runs against them)
+        lib.ss_model_last_source.restype = C.c_int
     lib.ss_kernel_time_log.argtypes = [vp, vp, C.c_int]
     lib.ss_kernel_time_log_k.argtypes = [vp, C.c_int, vp, C.c_int]
     if lib.ss_abi_version() != 1:
@@ -269,7 +270,8 @@ def model_check(params: Params | None = None):
     _check(lib.ss_model_check(C.byref(p), h, C.byref(qr)), "ss_model_check")
     return {"fk": f"{h[0]:016x}", "coef": f"{h[1]:016x}", "lhet": f"{h[2]:016x}", "q_r": qr.value,
             "pinned": bool(lib.ss_model_pinned(h)),
-            "source": {0: "built", 1: "process", 2: "disk"}.get(lib.ss_model_last_source(), "none")}
+            "source": {0: "built", 1: "process", 2: "disk"}.get(
+                lib.ss_model_last_source() if hasattr(lib, "ss_model_last_source") else -1, "none")}
 
 
 def synth_batch_host(synth: Synth, first_site: int, n_sites: int) -> Batch:
