@@ -259,7 +259,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.m.min_somatic_qual = c->hm.prm.min_somatic_qual;
     a.m.flags = (c->hm.prm.use_joint_priors ? SS_MF_JOINT : 0u) | (c->hm.prm.include_loh ? SS_MF_LOH : 0u) |
                 (c->hm.prm.include_gor ? SS_MF_GOR : 0u);
-    const int deep_grid = c->n_cu * 4;
+    const int deep_grid = c->n_cu * 3;              /* 3 blocks (12 one-site waves) per CU: LDS */
     c->last_stream = s;
     const hipEvent_t *evs = nullptr;
     if (c->timing && c->n_logged < 4096) {

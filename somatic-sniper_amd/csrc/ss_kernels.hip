@@ -19,9 +19,9 @@
  *   ss_score_wide   sites with 513..2048 sort slots (the main kernel lists
  *     them): the same packed network at 1024 / 2048 keys, 16 sites folded and
  *     finished together.
- *   ss_score_deep   one 256-thread block per site beyond that (any depth) or
- *     with malformed offsets: counting sort of the order-relevant key fields
- *     in LDS, then the same ordered fold, likelihood and decision code.
+ *   ss_score_deep   one wave per site beyond that (any depth) or with
+ *     malformed offsets: counting sort of the order-relevant key fields in
+ *     LDS windows, then the same ordered fold, likelihood and decision code.
  *
  * Bit-exactness: built with -ffp-contract=off (no FMA contraction); float
  * division and double sqrt are correctly rounded (sqrt re-checked with fma);
@@ -1630,29 +1630,35 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
  *   minq <  4:  minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz        0..127
  *   minq >= 4:  128 + (minq - 4) * 4 + hasbase * 2 + strand         128..1135
  * (for minq >= 4, E and nz only order reads of equal q and strand).
- * One 256-thread block per site builds both samples' histograms in LDS
- * (36 KB) and an occupancy bitmap; then 16 lanes of wave 0 -- (sample, base,
- * role) -- walk their group's bins from the top through the bitmap, folding
- * count-many steps per bin: the reference's serial chain, O(depth), with no
- * depth limit and no scratch memory.  The quads then evaluate the genotype
- * likelihoods and lane 0 decides the site.
+ *
+ * One wave per site, so a CU holds 12 sites at once.  A first pass over the
+ * site's reads finds its highest occupied bin and the rms sums.  The bins
+ * are then histogrammed in LDS one window of DW_BINS per group at a time,
+ * from the top down (one window when every read has minq <= 60); after each
+ * window 16 lanes -- (sample, base, role) -- walk their group's occupied
+ * bins downwards through a bitmap and fold count-many steps per bin,
+ * carrying the chain across windows: the reference's serial chain, O(depth),
+ * with no depth limit and no scratch memory.  The quads then evaluate the
+ * genotype likelihoods and lane 0 decides the site.
  * ------------------------------------------------------------------------ */
 namespace {
 
-#define DBIN 1136
-#define DBINS (2 * 4 * DBIN)
-#define DWORDS (DBINS / 32)
-static_assert(DBINS % 32 == 0, "bitmap words");
+#define DBIN 1136                       /* bins per group, all minq */
+#define DW_BINS 368                     /* bins per group in one LDS window */
+#define DW_HIST (8 * DW_BINS)
+#define DW_OCC (DW_HIST / 32)
+#define DEEP_WAVES (SS_DEEP_BLOCK / 64)
+static_assert(DW_HIST % 32 == 0 && DW_BINS % 4 == 0, "bitmap words");
 
-struct DeepLds {
-    uint32_t hist[DBINS];
-    uint32_t occ[DWORDS];
+struct DeepWave {
+    uint32_t hist[DW_HIST];
+    uint32_t occ[DW_OCC];
     unsigned long long rms[2];
     SlotRes res[2];
 };
 
-/* bin of one packed read within its sample's histogram, or SENT when its
- * clamped q is 0 (no contribution, sniper_maqcns.c:165-166) */
+/* group bin of one packed read, base << 16 | bin, or SENT when its clamped q
+ * is 0 (no contribution, sniper_maqcns.c:165-166) */
 __device__ __forceinline__ uint32_t deep_bin(uint32_t rd, uint32_t tb, uint32_t th)
 {
     const uint32_t bq = (rd >> 8) & 0xffu;
@@ -1664,7 +1670,7 @@ __device__ __forceinline__ uint32_t deep_bin(uint32_t rd, uint32_t tb, uint32_t 
     const uint32_t st = (rd >> 20) & 1u;
     const uint32_t idx = minq < 4u ? (minq << 5 | hb << 4 | st << 3 | (bq >> 6) << 1 | nz)
                                    : 128u + (minq - 4u) * 4u + hb * 2u + st;
-    return (minq | nz) != 0u ? base * DBIN + idx : SENT;
+    return (minq | nz) != 0u ? base << 16 | idx : SENT;
 }
 
 /* offsets of a site are usable iff they neither decrease nor pass the end of
@@ -1674,53 +1680,87 @@ __device__ __forceinline__ bool site_wellformed(uint32_t o0, uint32_t o1, uint32
     return o0 <= o1 && o1 <= end;
 }
 
-/* histogram one sample's reads; returns this thread's rms partial sum */
-__device__ __forceinline__ uint64_t deep_hist(const uint32_t *reads, uint32_t n, uint32_t tb, uint32_t th,
-                                              uint32_t cap, uint32_t *hist)
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
-    uint64_t rs = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t rd = __builtin_nontemporal_load(reads + i);
-        const uint32_t b = deep_bin(rd, tb, th);
-        if (b != SENT) atomicAdd(&hist[b], 1u);
-        const uint32_t t = min(rd & 0x7fu, cap);
-        rs += t * t;
-    }
-    return rs;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
 }
 
-/* ordered fold of one (sample, base) group from its histogram: acc gets
- * esum (role 0) or fsum (role 1), cnt the group size c[] (sniper_maqcns.c:160-172) */
-__device__ __forceinline__ void deep_fold(const uint32_t *hist, const uint32_t *occ, uint32_t lo,
-                                          const double *fk, uint32_t role, float &acc, uint32_t &cnt)
+/* one pass over one sample's reads, eight in flight per lane: mode 0 returns
+ * the highest bin + 1 over the reads and adds the rms terms to rs; mode 1
+ * counts the reads whose bin falls in [lo, hi) into the window histogram */
+template <int MODE>
+__device__ __forceinline__ uint32_t deep_pass(const uint32_t *reads, uint32_t n, uint32_t tb, uint32_t th,
+                                              uint32_t cap, uint32_t lo, uint32_t hi, uint32_t *hist,
+                                              uint64_t &rs)
 {
-    float e = 0.0f;
-    uint32_t w0 = 0, w1 = 0, c = 0;
-    const uint32_t hi = lo + DBIN;                 /* bins [lo, hi), walked downwards */
-    for (int wi = (int)((hi - 1u) >> 5); wi >= (int)(lo >> 5); --wi) {
+    const uint32_t lane = lane_id();
+    uint32_t top = 0;
+    for (uint64_t i = lane; i < n; i += 8u * 64u) {
+        uint32_t rd[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) {
+            const uint64_t ix = i + j * 64u;
+            rd[j] = ix < n ? __builtin_nontemporal_load(reads + ix) : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) {
+            const uint32_t b = deep_bin(rd[j], tb, th);
+            const uint32_t idx = b & 0xffffu;
+            if (MODE == 0) {
+                if (b != SENT) top = max(top, idx + 1u);
+                const uint32_t t = min(rd[j] & 0x7fu, cap);
+                rs += t * t;
+            } else if (b != SENT && idx >= lo && idx < hi) {
+                atomicAdd(&hist[(b >> 16) * DW_BINS + idx - lo], 1u);
+            }
+        }
+    }
+    return top;
+}
+
+/* ordered fold of one (sample, base) group over the window's bins [lo, hi),
+ * walked downwards; e, the two strand w counters and the count carry over
+ * from the window above (sniper_maqcns.c:160-172) */
+__device__ __forceinline__ void deep_fold(const uint32_t *hist, const uint32_t *occ, uint32_t gbin,
+                                          uint32_t lo, uint32_t hi, const double *fk, uint32_t role,
+                                          float &e, uint32_t &w0, uint32_t &w1, uint32_t &c)
+{
+    const uint32_t b_lo = gbin, b_hi = gbin + (hi - lo);   /* window slots of this group */
+    for (int wi = (int)((b_hi - 1u) >> 5); wi >= (int)(b_lo >> 5); --wi) {
         uint32_t bits = occ[wi];
         const uint32_t b0 = (uint32_t)wi * 32u;
-        if (b0 < lo) bits &= ~0u << (lo - b0);
-        if (b0 + 32u > hi) bits &= ~0u >> (b0 + 32u - hi);
+        if (b0 < b_lo) bits &= ~0u << (b_lo - b0);
+        if (b0 + 32u > b_hi) bits &= ~0u >> (b0 + 32u - b_hi);
         while (bits) {
             const uint32_t j = 31u - (uint32_t)__builtin_clz(bits);
             bits &= ~(1u << j);
-            const uint32_t idx = b0 + j - lo;
+            const uint32_t idx = b0 + j - b_lo + lo;        /* group bin */
             const uint32_t k = hist[b0 + j];
             const uint32_t q = idx < 128u ? max(idx >> 5, (idx & 1u) << 2) : (idx - 128u) / 4u + 4u;
             const uint32_t st = idx < 128u ? (idx >> 3) & 1u : idx & 1u;
             const double mul = role ? 1.0 : (double)q;
-            uint32_t w = st ? w1 : w0;
-            for (uint32_t r = 0; r < k; ++r) {
-                e = (float)((double)e + fk[w] * mul);
-                w = w < 255u ? w + 1u : 255u;
+            const uint32_t w = st ? w1 : w0;
+            /* batches of 8 steps: the eight fk[w] loads are issued before the
+             * dependent chain (w advances by one per read, saturating at 255);
+             * steps past the bin's count leave e unchanged */
+            for (uint32_t r = 0; r < k; r += 8u) {
+                double f[8];
+#pragma unroll
+                for (uint32_t t = 0; t < 8u; ++t) f[t] = fk[min(w + min(r, 256u) + t, 255u)];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (uint32_t t = 0; t < 8u; ++t) {
+                    const float en = (float)((double)e + f[t] * mul);
+                    e = r + t < k ? en : e;
+                }
             }
-            if (st) w1 = w; else w0 = w;
+            const uint32_t wn = min(w + min(k, 256u), 255u);
+            if (st) w1 = wn; else w0 = wn;
             c += k;
         }
     }
-    acc = e;
-    cnt = c;
 }
 
 }  // namespace
@@ -1728,79 +1768,89 @@ __device__ __forceinline__ void deep_fold(const uint32_t *hist, const uint32_t *
 __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
 {
     __shared__ double fk[256];
-    __shared__ DeepLds D;
+    __shared__ DeepWave DW[DEEP_WAVES];
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    DeepWave &D = DW[wv];
     const uint32_t count = *a.deep2_count;
     const uint32_t lim = count < a.deep_cap ? count : a.deep_cap;
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const uint32_t lane = lane_id();
-    for (uint32_t w = blockIdx.x; w < lim; w += gridDim.x) {
+    const uint32_t grp = ((lane >> 3) & 1u) * 4u + ((lane >> 1) & 3u);  /* fold lanes 0..15: sample, base */
+    for (uint32_t w = blockIdx.x * DEEP_WAVES + wv; w < lim; w += gridDim.x * DEEP_WAVES) {
         const uint32_t s = a.deep2_list[w];
         const uint32_t ot = a.off_t[s], ot1 = a.off_t[s + 1], on = a.off_n[s], on1 = a.off_n[s + 1];
         if (!site_wellformed(ot, ot1, end_t) || !site_wellformed(on, on1, end_n)) {
-            if (threadIdx.x == 0) {
+            if (lane == 0) {
                 atomicOr(a.err, SS_KERR_MALFORMED);
                 a.score[s] = -2;
             }
-            continue;                                  /* block-uniform */
+            continue;                                  /* wave-uniform */
         }
         const uint32_t nt = ot1 - ot, nn = on1 - on;
         const uint32_t refc = a.ref[s];
         const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
         uint32_t tb, th;
         nt_tables(ref16, tb, th);
-        for (uint32_t i = threadIdx.x; i < DBINS; i += blockDim.x) D.hist[i] = 0u;
-        if (threadIdx.x < 2u) D.rms[threadIdx.x] = 0ull;
-        __syncthreads();
-        const uint64_t rt = deep_hist(a.reads_t + ot, nt, tb, th, cap, D.hist);
-        const uint64_t rn = deep_hist(a.reads_n + on, nn, tb, th, cap, D.hist + 4 * DBIN);
+        if (lane < 2u) D.rms[lane] = 0ull;
+        wave_sync();
+        uint64_t rt = 0, rn = 0;
+        uint32_t top = max(deep_pass<0>(a.reads_t + ot, nt, tb, th, cap, 0, 0, D.hist, rt),
+                           deep_pass<0>(a.reads_n + on, nn, tb, th, cap, 0, 0, D.hist, rn));
+        top = wave_max(top);
         atomicAdd(&D.rms[0], (unsigned long long)rt);
         atomicAdd(&D.rms[1], (unsigned long long)rn);
-        __syncthreads();
-        for (uint32_t wd = threadIdx.x; wd < DWORDS; wd += blockDim.x) {
-            uint32_t bits = 0;
+        float acc = 0.0f;
+        uint32_t w0 = 0, w1 = 0, cnt = 0;
+        for (uint32_t hi = top; hi > 0u;) {            /* windows, top down (wave-uniform) */
+            const uint32_t lo = hi > DW_BINS ? hi - DW_BINS : 0u;
+            for (uint32_t i = lane; i < DW_HIST; i += 64u) D.hist[i] = 0u;
+            wave_sync();
+            uint64_t unused = 0;
+            deep_pass<1>(a.reads_t + ot, nt, tb, th, cap, lo, hi, D.hist, unused);
+            deep_pass<1>(a.reads_n + on, nn, tb, th, cap, lo, hi, D.hist + 4 * DW_BINS, unused);
+            wave_sync();
+            for (uint32_t wd = lane; wd < DW_OCC; wd += 64u) {
+                uint32_t bits = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < 32u; ++j) bits |= (D.hist[wd * 32u + j] != 0u ? 1u : 0u) << j;
-            D.occ[wd] = bits;
-        }
-        __syncthreads();
-        if (threadIdx.x < 64u) {
-            /* fold lanes 0..15: sample = lane >> 3, base = (lane >> 1) & 3, role = lane & 1 */
-            float acc = 0.0f;
-            uint32_t cnt = 0;
-            if (lane < 16u)
-                deep_fold(D.hist, D.occ, ((lane >> 3) * 4u + ((lane >> 1) & 3u)) * DBIN, fk, lane & 1u, acc, cnt);
-            /* lanes 0..3 finish the tumor, 4..7 the normal (quad-cooperative) */
-            const uint32_t smp = (lane >> 2) & 1u;
-            float es[4], fs[4];
-            uint32_t c[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int src = (int)(smp * 8u + 2u * (uint32_t)b);
-                es[b] = __shfl(acc, src);
-                fs[b] = __shfl(acc, src + 1);
-                c[b] = (uint32_t)__shfl((int)cnt, src);
-            }
-            const uint32_t n = smp ? nn : nt;
-            const uint64_t rms = D.rms[smp];
-            uint32_t lk[10], min_lk, rms_q, cns;
-            glf_and_cns((int)(lane & 3u), es, fs, c, n, rms, a.m, lk, min_lk, rms_q, cns);
-            if (lane == 0u || lane == 4u) {
-                SlotRes &r = D.res[smp];
-#pragma unroll
-                for (int g = 0; g < 10; ++g) r.lk[g] = (uint8_t)lk[g];
-                r.cns = cns;
-                r.depth = n > 16777215u ? 16777215u : n;
-                r.min_lk = (uint8_t)min_lk;
-                r.rms_q = (uint8_t)rms_q;
-                if (a.glf) store_glf(&a.glf[2ull * s + smp], ref16, lk, min_lk, rms_q, r.depth);
+                for (uint32_t j = 0; j < 32u; ++j) bits |= (D.hist[wd * 32u + j] != 0u ? 1u : 0u) << j;
+                D.occ[wd] = bits;
             }
             wave_sync();
-            if (lane == 0u) decide_site(a, s, refc | ref16 << 8, D.res[0], D.res[1]);
+            if (lane < 16u) deep_fold(D.hist, D.occ, grp * DW_BINS, lo, hi, fk, lane & 1u, acc, w0, w1, cnt);
+            wave_sync();
+            hi = lo;
         }
-        __syncthreads();
+        /* lanes 0..3 finish the tumor, 4..7 the normal (quad-cooperative) */
+        const uint32_t smp = (lane >> 2) & 1u;
+        float es[4], fs[4];
+        uint32_t c[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int src = (int)(smp * 8u + 2u * (uint32_t)b);
+            es[b] = __shfl(acc, src);
+            fs[b] = __shfl(acc, src + 1);
+            c[b] = (uint32_t)__shfl((int)cnt, src);
+        }
+        const uint32_t n = smp ? nn : nt;
+        const uint64_t rms = D.rms[smp];
+        uint32_t lk[10], min_lk, rms_q, cns;
+        glf_and_cns((int)(lane & 3u), es, fs, c, n, rms, a.m, lk, min_lk, rms_q, cns);
+        if (lane == 0u || lane == 4u) {
+            SlotRes &r = D.res[smp];
+#pragma unroll
+            for (int g = 0; g < 10; ++g) r.lk[g] = (uint8_t)lk[g];
+            r.cns = cns;
+            r.depth = n > 16777215u ? 16777215u : n;
+            r.min_lk = (uint8_t)min_lk;
+            r.rms_q = (uint8_t)rms_q;
+            if (a.glf) store_glf(&a.glf[2ull * s + smp], ref16, lk, min_lk, rms_q, r.depth);
+        }
+        wave_sync();
+        if (lane == 0u) decide_site(a, s, refc | ref16 << 8, D.res[0], D.res[1]);
+        wave_sync();
     }
 }
 

@@ -191,6 +191,25 @@ def test_many_deep_sites(pkg, oracle, ctx):
     ctx.check()
 
 
+def test_deep_windows_full_quality_range(pkg, oracle, ctx):
+    """Deep sites whose reads span mapQ and baseQ 0..255 (every bin of the
+    deep kernel's 1136 per group is reachable), both strands, every nt16 code:
+    the histogram is built and folded in several LDS windows from the top
+    down, the chain carried across them.  Depths straddle the window count
+    and the wide/deep boundary; one site has a single high-q read above a
+    bulk of low-q ones."""
+    rng = np.random.default_rng(77)
+    sites = []
+    for k, (nt_, nn_) in enumerate([(2100, 10), (2500, 1500), (40, 2600), (5000, 3000), (1030, 1030)]):
+        mk = lambda n: [pkg.pack_read(int(rng.integers(0, 256)), int(rng.integers(0, 256)),
+                                      int(rng.integers(0, 16)), int(rng.integers(0, 2))) for _ in range(n)]
+        sites.append(("ACGT"[k % 4], mk(nt_), mk(nn_)))
+    lowq = [pkg.pack_read(60, int(5 + i % 20), 1 + (i % 3), i & 1) for i in range(2400)]
+    sites.append(("A", lowq + [pkg.pack_read(250, 240, 8, 1)], lowq[:900]))
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), ctx=ctx)
+    ctx.check()
+
+
 def test_giant_parity(pkg, oracle, ctx):
     """> 4096 reads in a sample (the round-1 giant route) -> deep kernel."""
     big = pkg.synth_batch_host(pkg.Synth.default(6000, 4500, fixed_depth=1, **EXOTIC), 0, 6)
