@@ -1650,7 +1650,7 @@ namespace {
 #define DEEP_WAVES (SS_DEEP_BLOCK / 64)
 static_assert(DW_HIST % 32 == 0 && DW_BINS % 4 == 0, "bitmap words");
 
-struct DeepWave {
+struct alignas(16) DeepWave {
     uint32_t hist[DW_HIST];
     uint32_t occ[DW_OCC];
     unsigned long long rms[2];
@@ -1687,9 +1687,10 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
     return v;
 }
 
-/* one pass over one sample's reads, eight in flight per lane: mode 0 returns
- * the highest bin + 1 over the reads and adds the rms terms to rs; mode 1
- * counts the reads whose bin falls in [lo, hi) into the window histogram */
+/* one pass over one sample's reads, eight in flight per lane: counts the
+ * reads whose bin falls in [lo, hi) into the window histogram; mode 0 (the
+ * first pass, lo = 0, hi = DW_BINS) also returns the highest bin + 1 over the
+ * reads and adds the rms terms to rs */
 template <int MODE>
 __device__ __forceinline__ uint32_t deep_pass(const uint32_t *reads, uint32_t n, uint32_t tb, uint32_t th,
                                               uint32_t cap, uint32_t lo, uint32_t hi, uint32_t *hist,
@@ -1712,12 +1713,17 @@ __device__ __forceinline__ uint32_t deep_pass(const uint32_t *reads, uint32_t n,
                 if (b != SENT) top = max(top, idx + 1u);
                 const uint32_t t = min(rd[j] & 0x7fu, cap);
                 rs += t * t;
-            } else if (b != SENT && idx >= lo && idx < hi) {
-                atomicAdd(&hist[(b >> 16) * DW_BINS + idx - lo], 1u);
             }
+            if (b != SENT && idx >= lo && idx < hi) atomicAdd(&hist[(b >> 16) * DW_BINS + idx - lo], 1u);
         }
     }
     return top;
+}
+
+__device__ __forceinline__ void deep_zero(uint32_t *hist)
+{
+    uint4 *h4 = reinterpret_cast<uint4 *>(hist);
+    for (uint32_t i = lane_id(); i < DW_HIST / 4u; i += 64u) h4[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 /* ordered fold of one (sample, base) group over the window's bins [lo, hi),
@@ -1744,8 +1750,20 @@ __device__ __forceinline__ void deep_fold(const uint32_t *hist, const uint32_t *
             const uint32_t w = st ? w1 : w0;
             /* batches of 8 steps: the eight fk[w] loads are issued before the
              * dependent chain (w advances by one per read, saturating at 255);
-             * steps past the bin's count leave e unchanged */
-            for (uint32_t r = 0; r < k; r += 8u) {
+             * full batches first, then one masked batch for the rest of the
+             * bin.  Measured slower: adding +0.0 for masked steps instead of
+             * the select, batches of 16, and loading the next batch during
+             * the current chain. */
+            uint32_t r = 0;
+            for (; r + 8u <= k; r += 8u) {
+                double f[8];
+#pragma unroll
+                for (uint32_t t = 0; t < 8u; ++t) f[t] = fk[min(w + min(r, 256u) + t, 255u)];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (uint32_t t = 0; t < 8u; ++t) e = (float)((double)e + f[t] * mul);
+            }
+            if (r < k) {
                 double f[8];
 #pragma unroll
                 for (uint32_t t = 0; t < 8u; ++t) f[t] = fk[min(w + min(r, 256u) + t, 255u)];
@@ -1795,27 +1813,40 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
         uint32_t tb, th;
         nt_tables(ref16, tb, th);
         if (lane < 2u) D.rms[lane] = 0ull;
+        deep_zero(D.hist);
         wave_sync();
+        /* the first pass also counts the bottom window: when every bin is in
+         * it (minq <= 60 everywhere) it is the only pass */
         uint64_t rt = 0, rn = 0;
-        uint32_t top = max(deep_pass<0>(a.reads_t + ot, nt, tb, th, cap, 0, 0, D.hist, rt),
-                           deep_pass<0>(a.reads_n + on, nn, tb, th, cap, 0, 0, D.hist, rn));
+        uint32_t top = max(deep_pass<0>(a.reads_t + ot, nt, tb, th, cap, 0, DW_BINS, D.hist, rt),
+                           deep_pass<0>(a.reads_n + on, nn, tb, th, cap, 0, DW_BINS, D.hist + 4 * DW_BINS, rn));
         top = wave_max(top);
         atomicAdd(&D.rms[0], (unsigned long long)rt);
         atomicAdd(&D.rms[1], (unsigned long long)rn);
         float acc = 0.0f;
         uint32_t w0 = 0, w1 = 0, cnt = 0;
+        bool counted = top <= DW_BINS;
         for (uint32_t hi = top; hi > 0u;) {            /* windows, top down (wave-uniform) */
             const uint32_t lo = hi > DW_BINS ? hi - DW_BINS : 0u;
-            for (uint32_t i = lane; i < DW_HIST; i += 64u) D.hist[i] = 0u;
-            wave_sync();
-            uint64_t unused = 0;
-            deep_pass<1>(a.reads_t + ot, nt, tb, th, cap, lo, hi, D.hist, unused);
-            deep_pass<1>(a.reads_n + on, nn, tb, th, cap, lo, hi, D.hist + 4 * DW_BINS, unused);
+            if (!counted) {
+                wave_sync();
+                deep_zero(D.hist);
+                wave_sync();
+                uint64_t unused = 0;
+                deep_pass<1>(a.reads_t + ot, nt, tb, th, cap, lo, hi, D.hist, unused);
+                deep_pass<1>(a.reads_n + on, nn, tb, th, cap, lo, hi, D.hist + 4 * DW_BINS, unused);
+            }
+            counted = false;
             wave_sync();
             for (uint32_t wd = lane; wd < DW_OCC; wd += 64u) {
+                const uint4 *h4 = reinterpret_cast<const uint4 *>(D.hist + wd * 32u);
                 uint32_t bits = 0;
 #pragma unroll
-                for (uint32_t j = 0; j < 32u; ++j) bits |= (D.hist[wd * 32u + j] != 0u ? 1u : 0u) << j;
+                for (uint32_t j = 0; j < 8u; ++j) {
+                    const uint4 h = h4[j];
+                    bits |= (h.x != 0u ? 1u : 0u) << (4u * j) | (h.y != 0u ? 2u : 0u) << (4u * j) |
+                            (h.z != 0u ? 4u : 0u) << (4u * j) | (h.w != 0u ? 8u : 0u) << (4u * j);
+                }
                 D.occ[wd] = bits;
             }
             wave_sync();
