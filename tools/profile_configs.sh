@@ -1,6 +1,7 @@
 #!/bin/bash
 # Kernel-level evidence for the non-headline depth configurations (SURVEY.md
-# section 8d: C2 30x/30x, C3 100x/60x, C5 500x/500x): one bench line and one
+# section 8d: C2 30x/30x, C3 100x/60x, C5 500x/500x, plus a 1200x/1000x deep panel):
+# one bench line and one
 # rocprofv3 --kernel-trace --stats summary per configuration.
 #   bash tools/profile_configs.sh [TAG]      (through gpurun)
 set -euo pipefail
@@ -10,7 +11,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 export TMPDIR=/tmp
 # sites per step: as many as the u32 read offsets allow at that depth
-for cfg in "c2 30 30 67108864" "c3 100 60 33554432" "c5 500 500 1048576"; do
+for cfg in "c2 30 30 67108864" "c3 100 60 33554432" "c5 500 500 1048576" "d1200 1200 1000 262144"; do
   set -- $cfg
   name=$1; lt=$2; ln=$3; n=$4
   timeout -k 10 400 python3 "$R/bench.py" --no-cpu --steps 10 --warmup 2 --lt "$lt" --ln "$ln" --sites "$n" \
