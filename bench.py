@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """bench.py -- pileup sites/sec of the MI355X somatic scorer (BASELINE.json metric).
 
-One STEP = one pass of the scoring path (ss_score_batch_device: main + deep +
-giant kernels) over one HBM-resident batch of synthetic 60xT/30xN pileup sites
+One STEP = one pass of the scoring path (ss_score_batch_device: main + wide +
+deep kernels) over one HBM-resident batch of synthetic 60xT/30xN pileup sites
 (Poisson depths).  Inputs are generated on the device before
 timing; the timed region contains only scoring.
 

@@ -22,7 +22,7 @@
 #include "ss_kernels.h"
 #include "ss_synth.h"
 
-#define SS_EV_PER_LAUNCH 4   /* before main, after main, after wide, after deep + giant */
+#define SS_EV_PER_LAUNCH 4   /* before main, after main, after wide, after deep */
 
 struct ss_ctx {
     int device;
