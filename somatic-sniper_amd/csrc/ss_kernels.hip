@@ -570,23 +570,38 @@ __device__ __forceinline__ uint32_t key_to_rec(uint32_t k)
     return q | 1u << 16 | (k & 8u) << 25;
 }
 
-/* 16-bit fold record (wide kernel, whose LDS arena holds 16 deep sites):
- *   bits 0..7 q | bit 12 strand | bit 13 1 (fsum multiplier);
- * (r >> 8) & 31 is strand << 4 like the u32 record's top byte. */
-__device__ __forceinline__ uint32_t key_to_rec16(uint32_t k)
+/* 8-bit fold record (wide kernel: twice the sites of a 16-bit record in the
+ * same LDS arena, so a sub-group fills the 16 sites of the fold), for sites
+ * whose contributing reads all have minq < 64 (wide_q_fits):
+ *   bits 0..5 q | bit 6 strand | bit 7 1 (fsum multiplier);
+ * (r >> 2) & 16 is strand << 4 like the u32 record's top byte. */
+__device__ __forceinline__ uint32_t key_to_rec8(uint32_t k)
 {
     const uint32_t q = max((k >> 5) & 0xffu, (k & 1u) << 2);
-    return q | (k & 8u) << 9 | 1u << 13;
+    return q | (k & 8u) << 3 | 1u << 7;
+}
+
+/* every contributing key of the lane's registers has minq < 64 (key bits 11, 12 clear) */
+template <int K>
+__device__ __forceinline__ bool wide_q_fits(const uint32_t (&v)[1][K])
+{
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        const uint32_t lo = v[0][r] & 0xffffu, hi = v[0][r] >> 16;
+        ok = ok && (lo == 0xffffu || (lo & 0x1800u) == 0u) && (hi == 0xffffu || (hi & 0x1800u) == 0u);
+    }
+    return ok;
 }
 
 template <typename RecT> struct RecForm;
 template <> struct RecForm<uint32_t> {
     static __device__ __forceinline__ uint32_t shift(uint32_t r) { return r >> 24; }
-    static constexpr uint32_t ONE_BIT = 16u;
+    static constexpr uint32_t ONE_BIT = 16u, QBITS = 8u;
 };
-template <> struct RecForm<uint16_t> {
-    static __device__ __forceinline__ uint32_t shift(uint32_t r) { return (r >> 8) & 31u; }
-    static constexpr uint32_t ONE_BIT = 13u;
+template <> struct RecForm<uint8_t> {
+    static __device__ __forceinline__ uint32_t shift(uint32_t r) { return (r >> 2) & 16u; }
+    static constexpr uint32_t ONE_BIT = 7u, QBITS = 6u;
 };
 
 __device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b)
@@ -853,6 +868,50 @@ struct SiteA {
     uint32_t bt, nt, bn, nn, ref16;
 };
 
+/* Group sizes (sample, base) do not depend on the order, so they are counted
+ * from the keys before the sort, next to the rms sums: each contributing key
+ * adds one to its base's field of a per-lane counter (8-bit fields when a
+ * sample has at most 128 sort slots, K = 1; else 16-bit fields, two words),
+ * and one wave reduction per word replaces the eight ballot-and-popcount
+ * boundary counts over the sorted network. */
+template <int K>
+struct GroupCount {
+    static constexpr bool NARROW = K == 1;
+    static constexpr int NW = NARROW ? 1 : 2;
+    uint32_t t[NW], n[NW];        /* per-lane partial counts: tumor, normal */
+    __device__ __forceinline__ void zero()
+    {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) t[i] = n[i] = 0u;
+    }
+    /* the lane's key pair (k0, k1) of one sample; 0xffff (pad or q = 0) adds nothing */
+    __device__ __forceinline__ void add(uint32_t k0, uint32_t k1, bool tum)
+    {
+        uint32_t inc[NW];
+        if constexpr (NARROW) {
+            inc[0] = (k0 != 0xffffu ? 1u << ((k0 >> 10) & 0x18u) : 0u) +      /* 8 * base */
+                     (k1 != 0xffffu ? 1u << ((k1 >> 10) & 0x18u) : 0u);
+        } else {
+            const uint32_t o0 = k0 != 0xffffu ? 1u << ((k0 >> 9) & 16u) : 0u; /* 16 * (base & 1) */
+            const uint32_t o1 = k1 != 0xffffu ? 1u << ((k1 >> 9) & 16u) : 0u;
+            const bool h0 = (k0 >> 14) & 1u, h1 = (k1 >> 14) & 1u;
+            inc[0] = (h0 ? 0u : o0) + (h1 ? 0u : o1);
+            inc[1] = (h0 ? o0 : 0u) + (h1 ? o1 : 0u);
+        }
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            t[i] += tum ? inc[i] : 0u;
+            n[i] += tum ? 0u : inc[i];
+        }
+    }
+    /* base b's count from reduced words */
+    static __device__ __forceinline__ uint32_t field(const uint32_t *w, int b)
+    {
+        if constexpr (NARROW) return (w[0] >> (8 * b)) & 0xffu;
+        else return (w[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+    }
+};
+
 template <int K, int M>
 __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M], uint32_t cap,
                                            Slot3 *slot, Stamps &st)
@@ -860,6 +919,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
     const uint32_t lane = lane_id();
     uint32_t v[M][K];
     uint32_t rs_t[M], rs_n[M];
+    GroupCount<K> gc[M];
     /* input placement (the two elements of a lane are adjacent reads of ONE
      * sample and come from LDS with one ds_read2; a pad element is invalid) */
     bool split = true;
@@ -871,6 +931,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
         uint32_t tb, th;
         nt_tables(S[m].ref16, tb, th);
         uint32_t a_t = 0, a_n = 0;
+        gc[m].zero();
 #pragma unroll
         for (int r = 0; r < K; ++r) {
             /* i0: index of the lane's first read within its sample.  Split:
@@ -894,6 +955,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             const uint32_t x = (in0 ? t0 * t0 : 0u) + (in1 ? t1 * t1 : 0u);
             a_t += tum ? x : 0u;                      /* tumor part (non-split) */
             a_n += x;                                 /* both samples */
+            gc[m].add(k0, k1, tum);
             v[m][r] = k0 | k1 << 16;
         }
         rs_t[m] = a_t;
@@ -908,11 +970,25 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
 #pragma unroll
     for (int m = 0; m < M; ++m) {
         const uint32_t nt = S[m].nt, nn = S[m].nn, bt = S[m].bt, bn = S[m].bn;
-        /* group boundaries (sample, base) */
-        const uint32_t c1 = count_below<K>(v[m], 1u << 13), c2 = count_below<K>(v[m], 2u << 13);
-        const uint32_t c3 = count_below<K>(v[m], 3u << 13), c4 = count_below<K>(v[m], 4u << 13);
-        const uint32_t c5 = count_below<K>(v[m], 5u << 13), c6 = count_below<K>(v[m], 6u << 13);
-        const uint32_t c7 = count_below<K>(v[m], 7u << 13), c8 = count_below<K>(v[m], 0xffffu);
+        /* group sizes (sample, base), counted before the sort, and the
+         * boundaries c1..c8 of the groups in the sorted network */
+        constexpr int NW = GroupCount<K>::NW;
+        uint32_t wt[NW], wn[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            if (split) {                  /* one sample per half-wave */
+                const uint32_t h = wave_halfsums(gc[m].t[i] + gc[m].n[i]);
+                wt[i] = (uint32_t)__builtin_amdgcn_readlane((int)h, 31);
+                wn[i] = (uint32_t)__builtin_amdgcn_readlane((int)h, 63);
+            } else {
+                wt[i] = wave_sum(gc[m].t[i]);
+                wn[i] = wave_sum(gc[m].n[i]);
+            }
+        }
+        const uint32_t c1 = GroupCount<K>::field(wt, 0), c2 = c1 + GroupCount<K>::field(wt, 1);
+        const uint32_t c3 = c2 + GroupCount<K>::field(wt, 2), c4 = c3 + GroupCount<K>::field(wt, 3);
+        const uint32_t c5 = c4 + GroupCount<K>::field(wn, 0), c6 = c5 + GroupCount<K>::field(wn, 1);
+        const uint32_t c7 = c6 + GroupCount<K>::field(wn, 2), c8 = c7 + GroupCount<K>::field(wn, 3);
         st.mark(9);
         /* fold records back over the staged reads: tumor run, normal run */
         if (split) {
@@ -982,7 +1058,7 @@ __device__ __forceinline__ void fold_sample(const RecT *rec, const uint32_t cnt[
                                             const double *fk, uint32_t role, float acc[4])
 {
     const uint32_t start1 = cnt[0], start2 = cnt[0] + cnt[1], start3 = start2 + cnt[2];
-    const uint32_t moff = role ? RecForm<RecT>::ONE_BIT : 0u, mwid = role ? 1u : 8u;
+    const uint32_t moff = role ? RecForm<RecT>::ONE_BIT : 0u, mwid = role ? 1u : RecForm<RecT>::QBITS;
     const char *fkb = reinterpret_cast<const char *>(fk);
     uint32_t L = 0;
 #pragma unroll
@@ -1434,11 +1510,11 @@ void ss_score_main(ss_score_args a)
 namespace {
 
 #define WIDE_WAVES (SS_WIDE_BLOCK / 64)
-#define WIDE_LDS_U16 73728                 /* u16 fold records per workgroup: 144 KB of LDS */
-#define WIDE_ARENA (WIDE_LDS_U16 / WIDE_WAVES)      /* per wave */
+#define WIDE_LDS_REC 147456                /* u8 fold records per workgroup: 144 KB of LDS */
+#define WIDE_ARENA (WIDE_LDS_REC / WIDE_WAVES)      /* per wave (< 2^16: Slot3 rec_n) */
 
 struct WideLds {
-    uint16_t arena[WIDE_WAVES][WIDE_ARENA];
+    uint8_t arena[WIDE_WAVES][WIDE_ARENA];
     Slot3    slot[WIDE_WAVES][2 * GB];
     SlotRes  res[WIDE_WAVES][2 * GB];
     uint32_t site[WIDE_WAVES][GB];
@@ -1481,9 +1557,11 @@ __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite
     }
 }
 
+/* false (nothing written) when a contributing read has minq >= 64: the
+ * 8-bit record cannot hold its q, and the site goes to the deep kernel */
 template <int K>
-__device__ __forceinline__ void sort_site_wide(const uint32_t (&rd)[32], const WideSite &w, uint32_t ref16,
-                                               uint32_t cap, uint16_t *arena, uint32_t base, Slot3 *st2)
+__device__ __forceinline__ bool sort_site_wide(const uint32_t (&rd)[32], const WideSite &w, uint32_t ref16,
+                                               uint32_t cap, uint8_t *arena, uint32_t base, Slot3 *st2)
 {
     const uint32_t lane = lane_id();
     const uint32_t nt = w.nt, nn = w.nn, ntr = nt + (nt & 1u);
@@ -1491,6 +1569,8 @@ __device__ __forceinline__ void sort_site_wide(const uint32_t (&rd)[32], const W
     nt_tables(ref16, tb, th);
     uint32_t v[1][K];
     uint32_t a_t = 0, a_n = 0;
+    GroupCount<K> gc;
+    gc.zero();
 #pragma unroll
     for (int r = 0; r < K; ++r) {
         const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
@@ -1502,15 +1582,24 @@ __device__ __forceinline__ void sort_site_wide(const uint32_t (&rd)[32], const W
         const uint32_t x = t0 * t0 + t1 * t1;
         a_t += tum ? x : 0u;
         a_n += tum ? 0u : x;
+        gc.add(k0, k1, tum);
         v[0][r] = k0 | k1 << 16;
+    }
+    if (__ballot(!wide_q_fits<K>(v))) return false;
+    /* group sizes before the sort (see GroupCount) */
+    uint32_t wt[2], wn[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        wt[i] = wave_sum(gc.t[i]);
+        wn[i] = wave_sum(gc.n[i]);
     }
     if (SS_PRIO_WIDE) __builtin_amdgcn_s_setprio(SS_PRIO_WIDE);
     packed_bitonic_flip<1, K>(v, !w.split);
     if (SS_PRIO_WIDE) __builtin_amdgcn_s_setprio(0);
-    const uint32_t c1 = count_below<K>(v[0], 1u << 13), c2 = count_below<K>(v[0], 2u << 13);
-    const uint32_t c3 = count_below<K>(v[0], 3u << 13), c4 = count_below<K>(v[0], 4u << 13);
-    const uint32_t c5 = count_below<K>(v[0], 5u << 13), c6 = count_below<K>(v[0], 6u << 13);
-    const uint32_t c7 = count_below<K>(v[0], 7u << 13), c8 = count_below<K>(v[0], 0xffffu);
+    const uint32_t c1 = GroupCount<K>::field(wt, 0), c2 = c1 + GroupCount<K>::field(wt, 1);
+    const uint32_t c3 = c2 + GroupCount<K>::field(wt, 2), c4 = c3 + GroupCount<K>::field(wt, 3);
+    const uint32_t c5 = c4 + GroupCount<K>::field(wn, 0), c6 = c5 + GroupCount<K>::field(wn, 1);
+    const uint32_t c7 = c6 + GroupCount<K>::field(wn, 2), c8 = c7 + GroupCount<K>::field(wn, 3);
     /* records of both samples are written contiguously: [tumor groups][normal groups] */
     const uint32_t nb = w.split ? 64u * K : c4;
 #pragma unroll
@@ -1520,7 +1609,7 @@ __device__ __forceinline__ void sort_site_wide(const uint32_t (&rd)[32], const W
             const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
             const bool tum = e < nb;
             if (e < (tum ? c4 : nb + (c8 - c4)))
-                arena[base + (tum ? e : e - nb + c4)] = (uint16_t)key_to_rec16((v[0][r] >> (16 * h)) & 0xffffu);
+                arena[base + (tum ? e : e - nb + c4)] = (uint8_t)key_to_rec8((v[0][r] >> (16 * h)) & 0xffffu);
         }
     const uint32_t rms_t = wave_sum(a_t), rms_n = wave_sum(a_n);
     if (lane == 0) {
@@ -1533,6 +1622,7 @@ __device__ __forceinline__ void sort_site_wide(const uint32_t (&rd)[32], const W
         st2[1].cnt23 = (c7 - c6) | (c8 - c7) << 16;
         st2[1].rms = rms_n;
     }
+    return true;
 }
 
 }  // namespace
@@ -1545,7 +1635,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   /* wave-uniform */
-    uint16_t *arena = L.arena[wv];
+    uint8_t *arena = L.arena[wv];
     Slot3 *slot = L.slot[wv];
     SlotRes *res = L.res[wv];
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
@@ -1591,7 +1681,10 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                     wide_load(a, w_cur, rd);
                 }
                 ++i;
-                if (w.over) {
+                const uint32_t ref16 = w.ref >> 8;
+                const bool fits = !w.over && (slots <= 1024u ? sort_site_wide<8>(cur, w, ref16, cap, arena, used, slot + 2 * G)
+                                                             : sort_site_wide<16>(cur, w, ref16, cap, arena, used, slot + 2 * G));
+                if (!fits) {
                     if (lane == 0) {
                         const uint32_t d = atomicAdd(a.deep2_count, 1u);
                         if (d < a.deep_cap) a.deep2_list[d] = s;
@@ -1599,11 +1692,6 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                     }
                     continue;
                 }
-                const uint32_t ref16 = w.ref >> 8;
-                if (slots <= 1024u)
-                    sort_site_wide<8>(cur, w, ref16, cap, arena, used, slot + 2 * G);
-                else
-                    sort_site_wide<16>(cur, w, ref16, cap, arena, used, slot + 2 * G);
                 if (lane == 0) {
                     sites[G] = s;
                     refcs[G] = w.ref;
@@ -1613,7 +1701,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
             }
             wave_sync();
             Stamps nost;
-            if (G) finish_sub<uint16_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, nost);
+            if (G) finish_sub<uint8_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, nost);
         }
     }
 }
