@@ -1513,7 +1513,7 @@ namespace {
 #define WIDE_LDS_REC 147456                /* u8 fold records per workgroup: 144 KB of LDS */
 #define WIDE_ARENA (WIDE_LDS_REC / WIDE_WAVES)      /* per wave (< 2^16: Slot3 rec_n) */
 
-struct WideLds {
+struct alignas(16) WideLds {
     uint8_t arena[WIDE_WAVES][WIDE_ARENA];
     Slot3    slot[WIDE_WAVES][2 * GB];
     SlotRes  res[WIDE_WAVES][2 * GB];
@@ -1557,10 +1557,12 @@ __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite
     }
 }
 
-/* false (nothing written) when a contributing read has minq >= 64: the
- * 8-bit record cannot hold its q, and the site goes to the deep kernel */
+/* Returns the arena bytes the site's records take (a multiple of 2K, the
+ * lane's share), or -1 (nothing written) when a contributing read has
+ * minq >= 64: the 8-bit record cannot hold its q, and the site goes to the
+ * deep kernel. */
 template <int K>
-__device__ __forceinline__ bool sort_site_wide(const uint32_t (&rd)[32], const WideSite &w, uint32_t ref16,
+__device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const WideSite &w, uint32_t ref16,
                                                uint32_t cap, uint8_t *arena, uint32_t base, Slot3 *st2)
 {
     const uint32_t lane = lane_id();
@@ -1585,7 +1587,7 @@ __device__ __forceinline__ bool sort_site_wide(const uint32_t (&rd)[32], const W
         gc.add(k0, k1, tum);
         v[0][r] = k0 | k1 << 16;
     }
-    if (__ballot(!wide_q_fits<K>(v))) return false;
+    if (__ballot(!wide_q_fits<K>(v))) return -1;
     /* group sizes before the sort (see GroupCount) */
     uint32_t wt[2], wn[2];
 #pragma unroll
@@ -1600,29 +1602,39 @@ __device__ __forceinline__ bool sort_site_wide(const uint32_t (&rd)[32], const W
     const uint32_t c3 = c2 + GroupCount<K>::field(wt, 2), c4 = c3 + GroupCount<K>::field(wt, 3);
     const uint32_t c5 = c4 + GroupCount<K>::field(wn, 0), c6 = c5 + GroupCount<K>::field(wn, 1);
     const uint32_t c7 = c6 + GroupCount<K>::field(wn, 2), c8 = c7 + GroupCount<K>::field(wn, 3);
-    /* records of both samples are written contiguously: [tumor groups][normal groups] */
+    /* The record of network element e goes to base + e: the lane's 2K
+     * elements are contiguous, so they leave as 16-byte stores.  The tumor
+     * groups start at base, the normal ones at base + nb; pad and q = 0
+     * elements land past each sample's groups and are never read.  Lanes
+     * wholly past the extent store nothing (the next site starts there). */
     const uint32_t nb = w.split ? 64u * K : c4;
+    const uint32_t extent = ((w.split ? nb + (c8 - c4) : c8) + 2u * K - 1u) & ~(2u * K - 1u);
+    if (lane * (2u * K) < extent) {
 #pragma unroll
-    for (int r = 0; r < K; ++r)
+        for (int q = 0; q < K / 8; ++q) {
+            uint32_t d[4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
-            const bool tum = e < nb;
-            if (e < (tum ? c4 : nb + (c8 - c4)))
-                arena[base + (tum ? e : e - nb + c4)] = (uint8_t)key_to_rec8((v[0][r] >> (16 * h)) & 0xffffu);
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t x = v[0][8 * q + 2 * j], y = v[0][8 * q + 2 * j + 1];
+                d[j] = key_to_rec8(x & 0xffffu) | key_to_rec8(x >> 16) << 8 |
+                       key_to_rec8(y & 0xffffu) << 16 | key_to_rec8(y >> 16) << 24;
+            }
+            *reinterpret_cast<uint4 *>(arena + base + lane * (2u * K) + 16u * (uint32_t)q) =
+                make_uint4(d[0], d[1], d[2], d[3]);
         }
+    }
     const uint32_t rms_t = wave_sum(a_t), rms_n = wave_sum(a_n);
     if (lane == 0) {
         st2[0].rec_n = base | nt << 16;
         st2[0].cnt01 = c1 | (c2 - c1) << 16;
         st2[0].cnt23 = (c3 - c2) | (c4 - c3) << 16;
         st2[0].rms = rms_t;
-        st2[1].rec_n = (base + c4) | nn << 16;
+        st2[1].rec_n = (base + nb) | nn << 16;
         st2[1].cnt01 = (c5 - c4) | (c6 - c5) << 16;
         st2[1].cnt23 = (c7 - c6) | (c8 - c7) << 16;
         st2[1].rms = rms_n;
     }
-    return true;
+    return (int)extent;
 }
 
 }  // namespace
@@ -1651,14 +1663,25 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
         uint32_t i = 0, s_cur = 0;
         WideSite w_cur = {0, 0, 0, 0, 0, false, false};
         uint32_t rd[32];
+        /* the chunk's descriptors, lane k = entry k, loaded at once (one
+         * exposed chain of dependent loads per chunk, not per site) */
+        uint32_t c_s = 0, c_ot = 0, c_ot1 = 0, c_on = 0, c_on1 = 0, c_ref = 0;
+        if (lane < nlist) {
+            c_s = list[first + lane];
+            c_ot = a.off_t[c_s];
+            c_ot1 = a.off_t[c_s + 1];
+            c_on = a.off_n[c_s];
+            c_on1 = a.off_n[c_s + 1];
+            const uint32_t rc = a.ref[c_s];
+            c_ref = rc | (uint32_t)ss_tab_nt16(a.m)[rc] << 8;
+        }
         auto describe = [&](uint32_t k, uint32_t &s, WideSite &w) {
-            s = list[first + k];
-            w.ot = a.off_t[s];
-            w.nt = a.off_t[s + 1] - w.ot;
-            w.on = a.off_n[s];
-            w.nn = a.off_n[s + 1] - w.on;
-            const uint32_t rc = a.ref[s];
-            w.ref = rc | (uint32_t)ss_tab_nt16(a.m)[rc] << 8;
+            s = rl(c_s, k);
+            w.ot = rl(c_ot, k);
+            w.nt = rl(c_ot1, k) - w.ot;
+            w.on = rl(c_on, k);
+            w.nn = rl(c_on1, k) - w.on;
+            w.ref = rl(c_ref, k);
             wide_place(w, end_t, end_n);
         };
         if (nlist) {
@@ -1672,7 +1695,10 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 const uint32_t s = s_cur;
                 const WideSite w = w_cur;
                 const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
-                if (used + slots > WIDE_ARENA && !w.over) break;   /* next sub-group */
+                /* the most arena the site can take (sort_site_wide's extent) */
+                const uint32_t kb = slots <= 1024u ? 16u : 32u;
+                const uint32_t bound = ((w.split ? 32u * kb + w.nn : slots) + kb - 1u) & ~(kb - 1u);
+                if (used + bound > WIDE_ARENA && !w.over) break;   /* next sub-group */
                 uint32_t cur[32];
 #pragma unroll
                 for (int k = 0; k < 32; ++k) cur[k] = rd[k];
@@ -1682,9 +1708,9 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 }
                 ++i;
                 const uint32_t ref16 = w.ref >> 8;
-                const bool fits = !w.over && (slots <= 1024u ? sort_site_wide<8>(cur, w, ref16, cap, arena, used, slot + 2 * G)
-                                                             : sort_site_wide<16>(cur, w, ref16, cap, arena, used, slot + 2 * G));
-                if (!fits) {
+                const int ext = w.over ? -1 : (slots <= 1024u ? sort_site_wide<8>(cur, w, ref16, cap, arena, used, slot + 2 * G)
+                                                              : sort_site_wide<16>(cur, w, ref16, cap, arena, used, slot + 2 * G));
+                if (ext < 0) {
                     if (lane == 0) {
                         const uint32_t d = atomicAdd(a.deep2_count, 1u);
                         if (d < a.deep_cap) a.deep2_list[d] = s;
@@ -1696,7 +1722,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                     sites[G] = s;
                     refcs[G] = w.ref;
                 }
-                used += slots;
+                used += (uint32_t)ext;
                 ++G;
             }
             wave_sync();
