@@ -65,13 +65,20 @@ def test_synthetic_parity(pkg, oracle, lt, ln, kw, opts):
     assert_parity(pkg, oracle, batch, opts)
 
 
-@pytest.mark.parametrize("lt,ln,fixed,n", [(300, 300, 0, 300), (700, 700, 1, 60), (500, 500, 0, 200),
-                                           (250, 270, 0, 400)])
-def test_deep_parity(pkg, oracle, ctx, lt, ln, fixed, n):
+@pytest.mark.parametrize("lt,ln,fixed,n,wild", [(300, 300, 0, 300, 0.05), (700, 700, 1, 60, 0.05),
+                                                (500, 500, 0, 200, 0.05), (250, 270, 0, 400, 0.05),
+                                                (300, 300, 0, 300, 0.0), (500, 500, 0, 200, 0.0),
+                                                (700, 700, 1, 60, 0.0), (600, 500, 0, 120, 0.0),
+                                                (500, 500, 0, 300, 0.0005)])
+def test_deep_parity(pkg, oracle, ctx, lt, ln, fixed, n, wild):
     """Sites beyond the main kernel's 512 sort slots -> wide kernel (and the
     deep kernel past 2048); > 255 reads per class saturates w, > 255 total
-    rescales c (Appendix A.4)."""
-    batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=fixed, **EXOTIC), 0, n)
+    rescales c (Appendix A.4).  The wide kernel's 8-bit fold records hold
+    q < 64, so a site with a read of minq >= 64 (wild qualities: baseQ / mapQ
+    up to 255) is scored by the deep kernel instead: wild = 0.05 sends every
+    wide site there, 0 none, 5e-4 about a quarter (mixed routing)."""
+    kw = dict(EXOTIC, p_wild_qual=wild)
+    batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=fixed, **kw), 0, n)
     assert_parity(pkg, oracle, batch, ctx=ctx)
 
 
