@@ -931,7 +931,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
         uint32_t tb, th;
         nt_tables(S[m].ref16, tb, th);
         uint32_t a_t = 0, a_n = 0;
-        gc[m].zero();
+        if constexpr (K == 1) gc[m].zero();
 #pragma unroll
         for (int r = 0; r < K; ++r) {
             /* i0: index of the lane's first read within its sample.  Split:
@@ -955,7 +955,7 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
             const uint32_t x = (in0 ? t0 * t0 : 0u) + (in1 ? t1 * t1 : 0u);
             a_t += tum ? x : 0u;                      /* tumor part (non-split) */
             a_n += x;                                 /* both samples */
-            gc[m].add(k0, k1, tum);
+            if constexpr (K == 1) gc[m].add(k0, k1, tum);
             v[m][r] = k0 | k1 << 16;
         }
         rs_t[m] = a_t;
@@ -970,25 +970,32 @@ __device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M],
 #pragma unroll
     for (int m = 0; m < M; ++m) {
         const uint32_t nt = S[m].nt, nn = S[m].nn, bt = S[m].bt, bn = S[m].bn;
-        /* group sizes (sample, base), counted before the sort, and the
-         * boundaries c1..c8 of the groups in the sorted network */
-        constexpr int NW = GroupCount<K>::NW;
-        uint32_t wt[NW], wn[NW];
-#pragma unroll
-        for (int i = 0; i < NW; ++i) {
+        /* boundaries c1..c8 of the (sample, base) groups in the sorted
+         * network: at K = 1 from the group sizes counted before the sort (8-bit
+         * fields, one word per sample); at K = 2, 4 by ballot over the sorted
+         * keys (a sample's 256 reads can overflow an 8-bit field, and two-word
+         * counts measured 1.8% slower at 100x/60x) */
+        uint32_t c1, c2, c3, c4, c5, c6, c7, c8;
+        if constexpr (K == 1) {
+            uint32_t wt[1], wn[1];
             if (split) {                  /* one sample per half-wave */
-                const uint32_t h = wave_halfsums(gc[m].t[i] + gc[m].n[i]);
-                wt[i] = (uint32_t)__builtin_amdgcn_readlane((int)h, 31);
-                wn[i] = (uint32_t)__builtin_amdgcn_readlane((int)h, 63);
+                const uint32_t h = wave_halfsums(gc[m].t[0] + gc[m].n[0]);
+                wt[0] = (uint32_t)__builtin_amdgcn_readlane((int)h, 31);
+                wn[0] = (uint32_t)__builtin_amdgcn_readlane((int)h, 63);
             } else {
-                wt[i] = wave_sum(gc[m].t[i]);
-                wn[i] = wave_sum(gc[m].n[i]);
+                wt[0] = wave_sum(gc[m].t[0]);
+                wn[0] = wave_sum(gc[m].n[0]);
             }
+            c1 = GroupCount<K>::field(wt, 0); c2 = c1 + GroupCount<K>::field(wt, 1);
+            c3 = c2 + GroupCount<K>::field(wt, 2); c4 = c3 + GroupCount<K>::field(wt, 3);
+            c5 = c4 + GroupCount<K>::field(wn, 0); c6 = c5 + GroupCount<K>::field(wn, 1);
+            c7 = c6 + GroupCount<K>::field(wn, 2); c8 = c7 + GroupCount<K>::field(wn, 3);
+        } else {
+            c1 = count_below<K>(v[m], 1u << 13); c2 = count_below<K>(v[m], 2u << 13);
+            c3 = count_below<K>(v[m], 3u << 13); c4 = count_below<K>(v[m], 4u << 13);
+            c5 = count_below<K>(v[m], 5u << 13); c6 = count_below<K>(v[m], 6u << 13);
+            c7 = count_below<K>(v[m], 7u << 13); c8 = count_below<K>(v[m], 0xffffu);
         }
-        const uint32_t c1 = GroupCount<K>::field(wt, 0), c2 = c1 + GroupCount<K>::field(wt, 1);
-        const uint32_t c3 = c2 + GroupCount<K>::field(wt, 2), c4 = c3 + GroupCount<K>::field(wt, 3);
-        const uint32_t c5 = c4 + GroupCount<K>::field(wn, 0), c6 = c5 + GroupCount<K>::field(wn, 1);
-        const uint32_t c7 = c6 + GroupCount<K>::field(wn, 2), c8 = c7 + GroupCount<K>::field(wn, 3);
         st.mark(9);
         /* fold records back over the staged reads: tumor run, normal run */
         if (split) {
@@ -1311,15 +1318,8 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
 #pragma unroll
         for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
     }
-    /* every fold record has been read: the next sub-group's reads may now
-     * stream into the stage while the likelihoods are computed */
     wave_sync();
     st.mark(3);
-    if (have_next) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue_dma(a, nxt, stage);
-    }
-    st.mark(11);
     /* exchange esum / fsum within the lane pair (DPP, all lanes active) */
     float es[4], fs[4];
 #pragma unroll
@@ -1342,6 +1342,16 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         p[t] = role ? o : mine[t];
         p[5 + t] = role ? mine[t] : o;
     }
+    /* Every fold record has been read and every likelihood gather has
+     * landed: the next sub-group's reads may now stream into the stage while
+     * the glf records and decisions are formed.  (Issued before the gathers,
+     * the DMA was waited for at the first gather: vmcnt drains in issue
+     * order.) */
+    if (have_next) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue_dma(a, nxt, stage);
+    }
+    st.mark(11);
     st.mark(12);
     if (act && role == 0u) {
         uint32_t lk[10], min_lk, rms_q, cns;
