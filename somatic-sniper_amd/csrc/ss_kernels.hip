@@ -1550,20 +1550,39 @@ __device__ __forceinline__ void wide_place(WideSite &w, uint32_t end_t, uint32_t
     w.split = k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn);
 }
 
+/* All 16 register pairs, whatever the site's network: choosing 8 or 16 by a
+ * branch put rd in scratch (measured 30% slower).  One base pointer and
+ * limit per lane (split) or two (otherwise): 5% faster at 500x/500x than a
+ * per-pair select of sample, index and pointer. */
 __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite &w, uint32_t (&rd)[32])
 {
     const uint32_t lane = lane_id();
-    const uint32_t ntr = w.nt + (w.nt & 1u);
+    if (w.split) {
+        /* lanes 0..31 the tumor, 32..63 the normal: one base pointer per lane */
+        const bool tl = lane < 32u;
+        const uint32_t *bp = tl ? a.reads_t + w.ot : a.reads_n + w.on;
+        const uint32_t lim = w.over ? 0u : (tl ? w.nt : w.nn);
+        const uint32_t i00 = (lane & 31u) * 2u;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;            /* as in sort_sites */
-        const uint32_t es = ((uint32_t)r * 32u + (lane & 31u)) * 2u;
-        const bool tum = w.split ? lane < 32u : e0 < ntr;
-        const uint32_t i0 = w.split ? es : (tum ? e0 : e0 - ntr);
-        const uint32_t *src = tum ? a.reads_t + w.ot + i0 : a.reads_n + w.on + i0;
-        const uint32_t lim = w.over ? 0u : (tum ? w.nt : w.nn);   /* nothing is loaded for an over site */
-        rd[2 * r] = i0 < lim ? __builtin_nontemporal_load(src) : 0u;
-        rd[2 * r + 1] = i0 + 1u < lim ? __builtin_nontemporal_load(src + 1) : 0u;
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t i0 = i00 + (uint32_t)r * 64u;
+            rd[2 * r] = i0 < lim ? __builtin_nontemporal_load(bp + i0) : 0u;
+            rd[2 * r + 1] = i0 + 1u < lim ? __builtin_nontemporal_load(bp + i0 + 1) : 0u;
+        }
+    } else {
+        /* element e: tumor read e below ntr, normal read e - ntr above */
+        const uint32_t ntr = w.nt + (w.nt & 1u);
+        const uint32_t *tp = a.reads_t + w.ot, *np = a.reads_n + w.on - ntr;
+        const uint32_t lt = w.over ? 0u : w.nt, ln = w.over ? 0u : ntr + w.nn;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;            /* as in sort_sites */
+            const bool tum = e0 < ntr;
+            const uint32_t *src = (tum ? tp : np) + e0;
+            const uint32_t lim = tum ? lt : ln;
+            rd[2 * r] = e0 < lim ? __builtin_nontemporal_load(src) : 0u;
+            rd[2 * r + 1] = e0 + 1u < lim ? __builtin_nontemporal_load(src + 1) : 0u;
+        }
     }
 }
 
