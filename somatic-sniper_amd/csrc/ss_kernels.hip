@@ -1505,17 +1505,21 @@ void ss_score_main(ss_score_args a)
 
 /* --------------------------------------------------------------------------
  * Wide kernel: the sites the main kernel left on the deep list (more than
- * PK_MAX sort slots, e.g. 500x/500x panels), up to SS_WIDE_MAXSLOTS slots.
+ * PK_MAX sort slots, e.g. 500x/500x panels) whose samples have at most
+ * SS_WIDE_MAXSLOTS reads each.
  *
  * One workgroup per CU, SS_WIDE_BLOCK / 64 independent waves sharing 144 KB
- * of LDS as per-wave arenas of 16-bit fold records.  A wave takes 16 list entries at a time and,
- * site by site, loads the packed reads straight from HBM into registers,
- * sorts them with the same packed bitonic network as the main kernel
- * (1024 or 2048 slots: K = 8 or 16 registers), and writes the fold records
- * of both samples contiguously into the arena.  Then the sites are folded
- * together -- lane = (site, sample, role), so the wave runs up to 64 serial
- * chains at once instead of one -- and finished by the main kernel's code.
- * Sites beyond SS_WIDE_MAXSLOTS go to the second deep list (ss_score_deep).
+ * of LDS as per-wave arenas of 8-bit fold records.  A wave takes 16 list
+ * entries at a time and, sort unit by sort unit, loads the packed reads
+ * straight from HBM into registers, sorts them with the same packed bitonic
+ * network as the main kernel (1024 or 2048 keys: K = 8 or 16 registers), and
+ * writes the fold records into the arena.  A unit is a whole site of at most
+ * SS_WIDE_MAXSLOTS sort slots (both samples in one network), else one of its
+ * samples (1200x/1000x panels).  Then the sites are folded together -- lane =
+ * (site, sample, role), so the wave runs up to 64 serial chains at once
+ * instead of one -- and finished by the main kernel's code.  Larger or
+ * malformed sites, and sites with a read of minq >= 64, go to the second
+ * deep list (ss_score_deep).
  * ------------------------------------------------------------------------ */
 namespace {
 
@@ -1538,16 +1542,35 @@ struct alignas(16) WideLds {
 struct WideSite {
     uint32_t ot, nt, on, nn;
     uint32_t ref;      /* ref char | nt16 code << 8, loaded with the offsets (one site ahead) */
-    bool split;        /* split placement (see split_fits): top level skipped */
-    bool over;         /* more than SS_WIDE_MAXSLOTS slots or malformed offsets: deep kernel */
+    uint32_t unit;     /* 0 the whole site, 1 its tumor, 2 its normal (sites past SS_WIDE_MAXSLOTS slots) */
+    uint32_t sp;       /* non-split placement: elements below sp are tumor reads, the rest normal */
+    bool split;        /* unit 0, split placement (see split_fits): top level skipped */
+    bool over;         /* a sample beyond SS_WIDE_MAXSLOTS reads or malformed offsets: deep kernel */
 };
 
 __device__ __forceinline__ void wide_place(WideSite &w, uint32_t end_t, uint32_t end_n)
 {
-    w.over = max(w.nt, w.nn) > SS_WIDE_MAXSLOTS || w.nt + (w.nt & 1u) + w.nn > SS_WIDE_MAXSLOTS ||
+    w.over = max(w.nt, w.nn) > SS_WIDE_MAXSLOTS ||
              w.ot + w.nt < w.ot || w.ot + w.nt > end_t || w.on + w.nn < w.on || w.on + w.nn > end_n;
-    const bool k8 = w.nt + (w.nt & 1u) + w.nn <= 1024u;      /* the network sort_site_wide picks */
-    w.split = k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn);
+    const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
+    w.unit = !w.over && slots > SS_WIDE_MAXSLOTS ? 1u : 0u;
+    w.sp = w.unit ? 0xffffu : w.nt + (w.nt & 1u);
+    const bool k8 = slots <= 1024u;                          /* the network sort_site_wide picks */
+    w.split = !w.unit && (k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn));
+}
+
+/* the normal unit of a site whose tumor unit w was */
+__device__ __forceinline__ WideSite wide_normal_unit(WideSite w)
+{
+    w.unit = 2u;
+    w.sp = 0u;
+    return w;
+}
+
+/* network size of a unit: reads it sorts (incl. the pad between samples) */
+__device__ __forceinline__ uint32_t wide_unit_slots(const WideSite &w)
+{
+    return w.unit == 0u ? w.nt + (w.nt & 1u) + w.nn : (w.unit == 1u ? w.nt : w.nn);
 }
 
 /* All 16 register pairs, whatever the site's network: choosing 8 or 16 by a
@@ -1570,14 +1593,17 @@ __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite
             rd[2 * r + 1] = i0 + 1u < lim ? __builtin_nontemporal_load(bp + i0 + 1) : 0u;
         }
     } else {
-        /* element e: tumor read e below ntr, normal read e - ntr above */
-        const uint32_t ntr = w.nt + (w.nt & 1u);
-        const uint32_t *tp = a.reads_t + w.ot, *np = a.reads_n + w.on - ntr;
-        const uint32_t lt = w.over ? 0u : w.nt, ln = w.over ? 0u : ntr + w.nn;
+        /* element e: tumor read e below sp, normal read e - sp above (a
+         * unit takes one sample: sp past every element, or 0).  The normal
+         * base is offset by -sp so that element e indexes it directly; for a
+         * tumor unit it is never dereferenced. */
+        const uint32_t sp = w.sp;
+        const uint32_t *tp = a.reads_t + w.ot, *np = a.reads_n + w.on - sp;
+        const uint32_t lt = w.over ? 0u : w.nt, ln = w.over ? 0u : sp + w.nn;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;            /* as in sort_sites */
-            const bool tum = e0 < ntr;
+            const bool tum = e0 < sp;
             const uint32_t *src = (tum ? tp : np) + e0;
             const uint32_t lim = tum ? lt : ln;
             rd[2 * r] = e0 < lim ? __builtin_nontemporal_load(src) : 0u;
@@ -1595,7 +1621,7 @@ __device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const Wi
                                                uint32_t cap, uint8_t *arena, uint32_t base, Slot3 *st2)
 {
     const uint32_t lane = lane_id();
-    const uint32_t nt = w.nt, nn = w.nn, ntr = nt + (nt & 1u);
+    const uint32_t nt = w.nt, nn = w.nn;
     uint32_t tb, th;
     nt_tables(ref16, tb, th);
     uint32_t v[1][K];
@@ -1605,7 +1631,7 @@ __device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const Wi
 #pragma unroll
     for (int r = 0; r < K; ++r) {
         const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
-        const bool tum = w.split ? lane < 32u : e0 < ntr;
+        const bool tum = w.split ? lane < 32u : e0 < w.sp;
         const uint32_t rd0 = rd[2 * r], rd1 = rd[2 * r + 1];
         const uint32_t sb = tum ? 0u : 0x8000u;
         const uint32_t k0 = read_key16(rd0, tb, th, sb), k1 = read_key16(rd1, tb, th, sb);
@@ -1653,11 +1679,14 @@ __device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const Wi
         }
     }
     const uint32_t rms_t = wave_sum(a_t), rms_n = wave_sum(a_n);
-    if (lane == 0) {
+    /* a sample unit fills only its sample's slot */
+    if (lane == 0 && w.unit != 2u) {
         st2[0].rec_n = base | nt << 16;
         st2[0].cnt01 = c1 | (c2 - c1) << 16;
         st2[0].cnt23 = (c3 - c2) | (c4 - c3) << 16;
         st2[0].rms = rms_t;
+    }
+    if (lane == 0 && w.unit != 1u) {
         st2[1].rec_n = (base + nb) | nn << 16;
         st2[1].cnt01 = (c5 - c4) | (c6 - c5) << 16;
         st2[1].cnt23 = (c7 - c6) | (c8 - c7) << 16;
@@ -1690,7 +1719,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
         const uint32_t nlist = scount - first < GB ? scount - first : GB;
         /* site i's reads are in flight while site i-1 is sorted */
         uint32_t i = 0, s_cur = 0;
-        WideSite w_cur = {0, 0, 0, 0, 0, false, false};
+        WideSite w_cur = {0, 0, 0, 0, 0, 0, 0, false, false};
         uint32_t rd[32];
         /* the chunk's descriptors, lane k = entry k, loaded at once (one
          * exposed chain of dependent loads per chunk, not per site) */
@@ -1717,41 +1746,59 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
             describe(0, s_cur, w_cur);
             wide_load(a, w_cur, rd);
         }
+        uint32_t ext_t = 0;             /* arena bytes of the current site's tumor unit */
+        bool dead = false;              /* that tumor unit sent the site to the deep list */
         while (i < nlist) {
             int G = 0;
             uint32_t used = 0;
             while (i < nlist) {
                 const uint32_t s = s_cur;
                 const WideSite w = w_cur;
-                const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
-                /* the most arena the site can take (sort_site_wide's extent) */
+                const uint32_t slots = wide_unit_slots(w);
+                /* the most arena the site can take (sort_site_wide's extents), checked where a site starts */
                 const uint32_t kb = slots <= 1024u ? 16u : 32u;
-                const uint32_t bound = ((w.split ? 32u * kb + w.nn : slots) + kb - 1u) & ~(kb - 1u);
-                if (used + bound > WIDE_ARENA && !w.over) break;   /* next sub-group */
+                const uint32_t bound = w.unit ? ((w.nt + 31u) & ~31u) + ((w.nn + 31u) & ~31u)
+                                              : ((w.split ? 32u * kb + w.nn : slots) + kb - 1u) & ~(kb - 1u);
+                if (w.unit != 2u && used + bound > WIDE_ARENA && !w.over) break;   /* next sub-group */
                 uint32_t cur[32];
 #pragma unroll
                 for (int k = 0; k < 32; ++k) cur[k] = rd[k];
-                if (i + 1 < nlist) {
-                    describe(i + 1, s_cur, w_cur);
+                if (w.unit == 1u) {                       /* next: the same site's normal */
+                    w_cur = wide_normal_unit(w);
                     wide_load(a, w_cur, rd);
+                } else {
+                    if (i + 1 < nlist) {
+                        describe(i + 1, s_cur, w_cur);
+                        wide_load(a, w_cur, rd);
+                    }
+                    ++i;
                 }
-                ++i;
+                if (w.unit == 2u && dead) {               /* already on the deep list */
+                    dead = false;
+                    continue;
+                }
                 const uint32_t ref16 = w.ref >> 8;
-                const int ext = w.over ? -1 : (slots <= 1024u ? sort_site_wide<8>(cur, w, ref16, cap, arena, used, slot + 2 * G)
-                                                              : sort_site_wide<16>(cur, w, ref16, cap, arena, used, slot + 2 * G));
+                const uint32_t base = used + (w.unit == 2u ? ext_t : 0u);
+                const int ext = w.over ? -1 : (slots <= 1024u ? sort_site_wide<8>(cur, w, ref16, cap, arena, base, slot + 2 * G)
+                                                              : sort_site_wide<16>(cur, w, ref16, cap, arena, base, slot + 2 * G));
                 if (ext < 0) {
                     if (lane == 0) {
                         const uint32_t d = atomicAdd(a.deep2_count, 1u);
                         if (d < a.deep_cap) a.deep2_list[d] = s;
                         else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
                     }
+                    dead = w.unit == 1u;
+                    continue;
+                }
+                if (w.unit == 1u) {                       /* the site completes with its normal unit */
+                    ext_t = (uint32_t)ext;
                     continue;
                 }
                 if (lane == 0) {
                     sites[G] = s;
                     refcs[G] = w.ref;
                 }
-                used += (uint32_t)ext;
+                used += (w.unit == 2u ? ext_t : 0u) + (uint32_t)ext;
                 ++G;
             }
             wave_sync();
