@@ -265,7 +265,7 @@ def cpu_model() -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sites", type=int, default=1 << 26, help="sites per batch (per step, per GPU)")
     ap.add_argument("--batches", type=int, default=2, help="distinct resident batches cycled per rank")
