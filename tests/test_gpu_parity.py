@@ -84,12 +84,17 @@ def test_deep_parity(pkg, oracle, ctx, lt, ln, fixed, n, wild):
 
 @pytest.mark.parametrize("lt,ln,fixed,n,wild", [(1200, 1000, 0, 60, 0.0), (1500, 600, 1, 30, 0.0),
                                                 (2000, 2000, 1, 12, 0.0), (2100, 100, 1, 8, 0.0),
-                                                (1200, 1000, 0, 40, 0.0005), (1030, 1030, 1, 20, 0.05)])
+                                                (1200, 1000, 0, 40, 0.0005), (1030, 1030, 1, 20, 0.05),
+                                                (700, 480, 1, 40, 0.0), (480, 1050, 1, 40, 0.0),
+                                                (1000, 300, 1, 40, 0.0), (560, 470, 0, 200, 0.0),
+                                                (560, 470, 0, 120, 0.0005)])
 def test_wide_sample_units_parity(pkg, oracle, ctx, lt, ln, fixed, n, wild):
     """Sites past 2048 sort slots whose samples have at most 2048 reads each:
     the wide kernel sorts each sample in a network of its own (sort units),
     K = 8 or 16 per sample; a sample beyond 2048 (2100/100) and sites with
-    wild qualities go to the deep kernel."""
+    wild qualities go to the deep kernel.  Sites past 1024 slots with one
+    sample of at most 512 reads (700/480, 480/1050, 1000/300, Poisson
+    560/470) are units too: K = 4 for the small sample, 8 for the other."""
     kw = dict(EXOTIC, p_wild_qual=wild)
     batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=fixed, **kw), 3, n)
     assert_parity(pkg, oracle, batch, ctx=ctx)

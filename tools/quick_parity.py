@@ -18,7 +18,7 @@ def main():
     pkg = load_package()
     print("library:", pkg.library_path())
     cfgs = [(60, 30, {}), (30, 30, EXOTIC), (100, 60, EXOTIC), (3, 2, dict(p_wild_qual=0.3, p_del=0.3)),
-            (200, 150, EXOTIC), (500, 500, EXOTIC), (700, 300, {})]
+            (200, 150, EXOTIC), (500, 500, EXOTIC), (700, 300, {}), (560, 470, dict(EXOTIC, p_wild_qual=0.0))]
     bad = 0
     for lt, ln, kw in cfgs:
         b = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=7, **kw), 0, 4000 if lt + ln < 500 else 1500)
