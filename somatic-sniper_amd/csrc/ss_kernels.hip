@@ -1515,7 +1515,8 @@ void ss_score_main(ss_score_args a)
  * network as the main kernel (1024 or 2048 keys: K = 8 or 16 registers), and
  * writes the fold records into the arena.  A unit is a whole site of at most
  * SS_WIDE_MAXSLOTS sort slots (both samples in one network), else one of its
- * samples (1200x/1000x panels).  Then the sites are folded together -- lane =
+ * samples (1200x/1000x panels; also past 1024 slots when one sample has at
+ * most 512 reads: K = 4 + K = 8 instead of one 2048-key network).  Then the sites are folded together -- lane =
  * (site, sample, role), so the wave runs up to 64 serial chains at once
  * instead of one -- and finished by the main kernel's code.  Larger or
  * malformed sites, and sites with a read of minq >= 64, go to the second
@@ -1542,7 +1543,7 @@ struct alignas(16) WideLds {
 struct WideSite {
     uint32_t ot, nt, on, nn;
     uint32_t ref;      /* ref char | nt16 code << 8, loaded with the offsets (one site ahead) */
-    uint32_t unit;     /* 0 the whole site, 1 its tumor, 2 its normal (sites past SS_WIDE_MAXSLOTS slots) */
+    uint32_t unit;     /* 0 the whole site, 1 its tumor, 2 its normal (see wide_place) */
     uint32_t sp;       /* non-split placement: elements below sp are tumor reads, the rest normal */
     bool split;        /* unit 0, split placement (see split_fits): top level skipped */
     bool over;         /* a sample beyond SS_WIDE_MAXSLOTS reads or malformed offsets: deep kernel */
@@ -1553,7 +1554,11 @@ __device__ __forceinline__ void wide_place(WideSite &w, uint32_t end_t, uint32_t
     w.over = max(w.nt, w.nn) > SS_WIDE_MAXSLOTS ||
              w.ot + w.nt < w.ot || w.ot + w.nt > end_t || w.on + w.nn < w.on || w.on + w.nn > end_n;
     const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
-    w.unit = !w.over && slots > SS_WIDE_MAXSLOTS ? 1u : 0u;
+    /* past 1024 slots with one sample of at most 512 reads: a 512-key and a
+     * 1024-key network (45 x 4 + 55 x 8 register stages) instead of one split
+     * 2048-key network (55 x 16) */
+    const bool small_unit = slots > 1024u && max(w.nt, w.nn) <= 1024u && min(w.nt, w.nn) <= 512u;
+    w.unit = !w.over && (slots > SS_WIDE_MAXSLOTS || small_unit) ? 1u : 0u;
     w.sp = w.unit ? 0xffffu : w.nt + (w.nt & 1u);
     const bool k8 = slots <= 1024u;                          /* the network sort_site_wide picks */
     w.split = !w.unit && (k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn));
@@ -1663,8 +1668,21 @@ __device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const Wi
      * elements land past each sample's groups and are never read.  Lanes
      * wholly past the extent store nothing (the next site starts there). */
     const uint32_t nb = w.split ? 64u * K : c4;
-    const uint32_t extent = ((w.split ? nb + (c8 - c4) : c8) + 2u * K - 1u) & ~(2u * K - 1u);
-    if (lane * (2u * K) < extent) {
+    /* extents stay multiples of 16 bytes: every unit's stores are 16-byte aligned */
+    constexpr uint32_t XR = K < 8 ? 16u : 2u * K;
+    const uint32_t extent = ((w.split ? nb + (c8 - c4) : c8) + XR - 1u) & ~(XR - 1u);
+    if constexpr (K == 4) {
+        if (lane * 8u < extent) {
+            uint32_t d[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t x = v[0][2 * j], y = v[0][2 * j + 1];
+                d[j] = key_to_rec8(x & 0xffffu) | key_to_rec8(x >> 16) << 8 |
+                       key_to_rec8(y & 0xffffu) << 16 | key_to_rec8(y >> 16) << 24;
+            }
+            *reinterpret_cast<uint2 *>(arena + base + lane * 8u) = make_uint2(d[0], d[1]);
+        }
+    } else if (lane * (2u * K) < extent) {
 #pragma unroll
         for (int q = 0; q < K / 8; ++q) {
             uint32_t d[4];
@@ -1779,8 +1797,10 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 }
                 const uint32_t ref16 = w.ref >> 8;
                 const uint32_t base = used + (w.unit == 2u ? ext_t : 0u);
-                const int ext = w.over ? -1 : (slots <= 1024u ? sort_site_wide<8>(cur, w, ref16, cap, arena, base, slot + 2 * G)
-                                                              : sort_site_wide<16>(cur, w, ref16, cap, arena, base, slot + 2 * G));
+                const int ext = w.over ? -1
+                              : w.unit && slots <= 512u ? sort_site_wide<4>(cur, w, ref16, cap, arena, base, slot + 2 * G)
+                              : slots <= 1024u ? sort_site_wide<8>(cur, w, ref16, cap, arena, base, slot + 2 * G)
+                                               : sort_site_wide<16>(cur, w, ref16, cap, arena, base, slot + 2 * G);
                 if (ext < 0) {
                     if (lane == 0) {
                         const uint32_t d = atomicAdd(a.deep2_count, 1u);
