@@ -1633,8 +1633,15 @@ __device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const Wi
     uint32_t a_t = 0, a_n = 0;
     GroupCount<K> gc;
     gc.zero();
+    /* registers whose elements are all pads (rd = 0: key 0xffff, no rms or
+     * count) skip the key build: a wave-uniform bound on the live elements */
+    const uint32_t live = w.split ? 2u * max(nt, nn) : wide_unit_slots(w);
 #pragma unroll
     for (int r = 0; r < K; ++r) {
+        if ((uint32_t)r * 128u >= live) {
+            v[0][r] = 0xffffffffu;
+            continue;
+        }
         const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
         const bool tum = w.split ? lane < 32u : e0 < w.sp;
         const uint32_t rd0 = rd[2 * r], rd1 = rd[2 * r + 1];
