@@ -27,7 +27,7 @@
  * usable GPU the program stops with an error.
  *
  * Environment: SS_DEVICE (GPU index, default 0), SS_DEVICES (comma list of GPU
- * indices, overrides SS_DEVICE), SS_BATCH (sites per batch,
+ * indices, overrides SS_DEVICE; SS_DEVICES_SHARED=1 allows repeats), SS_BATCH (sites per batch,
  * default 2^20), SS_BGZF_THREADS (inflate threads per BAM, default 4),
  * SS_PILEUP_THREADS (2, default: column pileup, per sample a reader thread and
  * SS_PILEUP_WORKERS (default 3) window builders;
@@ -120,7 +120,8 @@ typedef struct {
     uint64_t seq_fill;        /* batch the pileup is filling (= batches submitted) */
     uint64_t seq_claim;       /* next submitted batch a scorer takes */
     uint64_t seq_write;       /* next batch to be written (output order) */
-    int quit, failed;
+    int quit;
+    int failed;               /* set by any scorer, read by all threads: __atomic only (failed_get/set) */
     pthread_t th[MAX_DEV];
     pthread_mutex_t mu;
     pthread_cond_t cv;
@@ -137,6 +138,9 @@ typedef struct {
     int k;                    /* scorer index */
 } scorer_arg_t;
 
+static int failed_get(run_t *R) { return __atomic_load_n(&R->failed, __ATOMIC_ACQUIRE); }
+static void failed_set(run_t *R) { __atomic_store_n(&R->failed, 1, __ATOMIC_RELEASE); }
+
 /* score batch b on context ctx; returns the number of emitted calls or -1 */
 static long score_batch(run_t *R, ss_ctx_t *ctx, batch_t *b)
 {
@@ -152,7 +156,7 @@ static long score_batch(run_t *R, ss_ctx_t *ctx, batch_t *b)
         }
         if (rc) {
             fprintf(stderr, "[bam-somaticsniper] GPU scoring failed: %s\n", ss_strerror(rc));
-            R->failed = 1;
+            failed_set(R);
             return -1;
         }
         return (long)ncalls;
@@ -232,7 +236,7 @@ static void *scorer_main(void *arg)
         const uint64_t s = R->seq_claim++;
         batch_t *b = &R->bat[s % (uint64_t)R->n_bat];
         pthread_mutex_unlock(&R->mu);
-        const long ncalls = R->failed ? -1 : score_batch(R, ctx, b);
+        const long ncalls = failed_get(R) ? -1 : score_batch(R, ctx, b);
         stamp("batch scored");
         pthread_mutex_lock(&R->mu);
         while (R->seq_write != s) pthread_cond_wait(&R->cv, &R->mu);   /* output in batch order */
@@ -309,7 +313,7 @@ static int on_site(int32_t tid, int32_t pos, int n1, int n2, const uint32_t *pk1
         return 0;
     }
     if (b->n == b->cap || b->nt > 0xC0000000u || b->nn > 0xC0000000u) submit(R);
-    return R->failed;
+    return failed_get(R);
 }
 
 /* ---- command line --------------------------------------------------------- */
@@ -350,6 +354,40 @@ static int env_int(const char *name, int dflt)
 {
     const char *v = getenv(name);
     return v && *v ? atoi(v) : dflt;
+}
+
+/* SS_DEVICES: a comma list of distinct GPU indices (at most MAX_DEV).  An
+ * empty, non-numeric, negative or repeated entry, or too many entries, is an
+ * error: a typo must not silently put two scorers on one GPU.  Several
+ * scorers on one GPU on purpose (tests on a one-GPU host) need
+ * SS_DEVICES_SHARED=1 as well. */
+static int parse_devices(const char *s, int *dev, int *n)
+{
+    const char *sh = getenv("SS_DEVICES_SHARED");
+    const int shared = sh && sh[0] == '1';
+    const char *q = s;
+    *n = 0;
+    for (;;) {
+        char *end;
+        const long v = strtol(q, &end, 10);
+        if (end == q || v < 0 || v > 1023 || (*end != ',' && *end != 0)) {
+            fprintf(stderr, "[bam-somaticsniper] SS_DEVICES='%s': bad entry at '%s' (expected a comma list of "
+                            "GPU indices)\n", s, q);
+            return 1;
+        }
+        if (*n == MAX_DEV) {
+            fprintf(stderr, "[bam-somaticsniper] SS_DEVICES='%s': more than %d devices\n", s, MAX_DEV);
+            return 1;
+        }
+        for (int i = 0; i < *n && !shared; ++i)
+            if (dev[i] == (int)v) {
+                fprintf(stderr, "[bam-somaticsniper] SS_DEVICES='%s': device %ld listed twice\n", s, v);
+                return 1;
+            }
+        dev[(*n)++] = (int)v;
+        if (*end == 0) return 0;
+        q = end + 1;
+    }
 }
 
 int main(int argc, char *argv[])
@@ -430,13 +468,7 @@ int main(int argc, char *argv[])
     const int cap = env_int("SS_BATCH", 1 << 20);
     {   /* scorer devices: SS_DEVICES=0,1,.. or SS_DEVICE */
         const char *devs = getenv("SS_DEVICES");
-        if (devs && *devs) {
-            for (const char *q = devs; *q && R.n_dev < MAX_DEV;) {
-                R.device[R.n_dev++] = atoi(q);
-                while (*q && *q != ',') ++q;
-                if (*q == ',') ++q;
-            }
-        }
+        if (devs && *devs && parse_devices(devs, R.device, &R.n_dev)) return 1;
         if (R.n_dev == 0) R.device[R.n_dev++] = env_int("SS_DEVICE", 0);
     }
     R.n_bat = R.n_dev + 3;
@@ -473,5 +505,5 @@ int main(int argc, char *argv[])
     if (R.dump) fclose(R.dump);
     fclose(R.out);
     stamp("exit");
-    return R.failed ? 1 : 0;
+    return failed_get(&R) ? 1 : 0;
 }

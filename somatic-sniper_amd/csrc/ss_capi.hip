@@ -7,6 +7,15 @@
  *           (read-only, stays resident in L2/MALL after the first batches)
  *   lists   deep site lists + counters (sized from the batch)
  *   host-path staging buffers, grown on demand
+ *
+ * Contexts are independent (include/sniper_amd.h): nothing here waits for
+ * the whole device.  A context waits only for its own work -- its `done`
+ * event (the latest launch, whatever stream it went to) and its own stream
+ * -- and allocates and frees its device memory stream-ordered
+ * (hipMallocAsync / hipFreeAsync), because hipFree and hipHostFree imply a
+ * hipDeviceSynchronize that would make one context wait for another's
+ * kernels.  Page-locked staging memory is malloc'd and registered
+ * (hipHostRegister / hipHostUnregister) for the same reason.
  */
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -73,31 +82,62 @@ extern "C" const char *ss_strerror(int code)
     }
 }
 
-static int dev_alloc(void **p, size_t bytes)
+/* stream-ordered device allocation: usable on any stream once `s` has
+ * reached it (callers order their use after it) */
+static int dev_alloc(void **p, size_t bytes, hipStream_t s)
 {
-    if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) { *p = nullptr; return SS_E_NOMEM; }
+    if (hipMallocAsync(p, bytes ? bytes : 16, s) != hipSuccess) { *p = nullptr; return SS_E_NOMEM; }
     return SS_OK;
 }
 
-template <typename T>
-static int upload(T **dst, const T *src, size_t n)
+static void dev_free(void *&p, hipStream_t s)
 {
-    int rc = dev_alloc((void **)dst, n * sizeof(T));
-    if (rc) return rc;
-    HIPCHK(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
-    return SS_OK;
+    if (p) hipFreeAsync(p, s);
+    p = nullptr;
+}
+
+/* page-locked host memory without hipHostMalloc / hipHostFree (the free
+ * synchronizes the device) */
+static void *pinned_alloc(size_t bytes)
+{
+    void *p = nullptr;
+    if (posix_memalign(&p, 4096, bytes ? bytes : 1) != 0) return nullptr;
+    if (hipHostRegister(p, bytes ? bytes : 1, hipHostRegisterDefault) != hipSuccess) {
+        free(p);
+        return nullptr;
+    }
+    return p;
+}
+
+static void pinned_free(void *&p)
+{
+    if (p) {
+        hipHostUnregister(p);
+        free(p);
+    }
+    p = nullptr;
+}
+
+/* wait for this context's own work only: its latest launch and its stream */
+static void ctx_quiesce(ss_ctx_t *c)
+{
+    if (c->launched && c->done) hipEventSynchronize(c->done);
+    if (c->hstream) hipStreamSynchronize(c->hstream);
 }
 
 extern "C" void ss_ctx_destroy(ss_ctx_t *c)
 {
     if (!c) return;
     hipSetDevice(c->device);
-    hipDeviceSynchronize();
-    void *ptrs[] = {c->d_tab, c->d_counters, c->d_deep_list, c->d_deep_seg, c->d_stage, c->d_cdf, c->d_scan_tmp,
-                    c->d_depth_tmp};
-    for (void *p : ptrs)
-        if (p) hipFree(p);
-    if (c->h_stage) hipHostFree(c->h_stage);
+    ctx_quiesce(c);
+    if (c->hstream) {
+        void **ptrs[] = {(void **)&c->d_tab, (void **)&c->d_counters, (void **)&c->d_deep_list,
+                         (void **)&c->d_deep_seg, &c->d_stage, (void **)&c->d_cdf, &c->d_scan_tmp,
+                         (void **)&c->d_depth_tmp};
+        for (void **p : ptrs) dev_free(*p, c->hstream);
+        hipStreamSynchronize(c->hstream);
+    }
+    pinned_free(c->h_stage);
     if (c->ev) {
         for (hipEvent_t e : *c->ev) hipEventDestroy(e);
         delete c->ev;
@@ -124,8 +164,14 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { ss_ctx_destroy(c); return SS_E_HIP; }
     c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
+        ss_ctx_destroy(c);
+        return SS_E_HIP;
+    }
+    hipStream_t hs = c->hstream;
 #define TRY(x) do { if ((rc = (x)) != SS_OK) { ss_ctx_destroy(c); return rc; } } while (0)
-    TRY(dev_alloc((void **)&c->d_tab, SS_TAB_BYTES));
+    TRY(dev_alloc((void **)&c->d_tab, SS_TAB_BYTES, hs));
     {
         struct { size_t off; const void *src; size_t n; } parts[] = {
             {SS_TAB_COEF, c->hm.coef, ((size_t)64 << 16) * sizeof(double)},
@@ -137,18 +183,18 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
             {SS_TAB_NT16, ss_nt16_table, 256},
         };
         for (auto &pt : parts)
-            if (hipMemcpy(c->d_tab + pt.off, pt.src, pt.n, hipMemcpyHostToDevice) != hipSuccess) {
+            if (hipMemcpyAsync(c->d_tab + pt.off, pt.src, pt.n, hipMemcpyHostToDevice, hs) != hipSuccess) {
                 ss_ctx_destroy(c);
                 return SS_E_HIP;
             }
     }
-    TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t)));
-    TRY(dev_alloc((void **)&c->d_deep_seg, (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t)));
-    TRY(dev_alloc((void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t)));
+    TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t), hs));
+    TRY(dev_alloc((void **)&c->d_deep_seg, (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t), hs));
+    TRY(dev_alloc((void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t), hs));
 #undef TRY
-    if (hipMemset(c->d_counters, 0, 16 * sizeof(uint32_t)) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
+    /* the tables, lists and counters are complete before any launch can use them */
+    if (hipMemsetAsync(c->d_counters, 0, 16 * sizeof(uint32_t), hs) != hipSuccess ||
+        hipStreamSynchronize(hs) != hipSuccess) {
         ss_ctx_destroy(c);
         return SS_E_HIP;
     }
@@ -181,19 +227,17 @@ extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double
 }
 
 /* the deep list buffer holds two lists of deep_cap entries: the main
- * kernel's per-wave segments (deep) and the wide kernel's overflow (deep2) */
-static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites)
+ * kernel's per-wave segments (deep) and the wide kernel's overflow (deep2).
+ * Grown on the launch stream `s`, which has already waited for the
+ * context's previous launch (the last user of the old list). */
+static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
 {
     if (n_sites <= c->deep_cap) return SS_OK;
     uint64_t cap = std::max<uint64_t>(n_sites, 1u << 16);
     if (cap > 0xffffffffull) return SS_E_INVAL;
-    if (c->d_deep_list) {
-        hipDeviceSynchronize();
-        hipFree(c->d_deep_list);
-        c->d_deep_list = nullptr;
-    }
+    dev_free(*(void **)&c->d_deep_list, s);
     c->deep_cap = 0;
-    if (dev_alloc((void **)&c->d_deep_list, 2 * cap * sizeof(uint32_t))) return SS_E_NOMEM;
+    if (dev_alloc((void **)&c->d_deep_list, 2 * cap * sizeof(uint32_t), s)) return SS_E_NOMEM;
     c->deep_cap = (uint32_t)cap;
     return SS_OK;
 }
@@ -220,11 +264,11 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     if (blocks > max_blocks) blocks = max_blocks;
     const uint64_t nseg = blocks * (SS_MAIN_BLOCK / 64);
     const uint64_t seg_cap = (site_blocks + nseg - 1) / nseg * 16;
-    int rc = ensure_deep_cap(c, nseg * seg_cap);
-    if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
     /* one launch at a time per context (shared work lists and counters) */
     if (c->launched && s != c->last_stream) HIPCHK(hipStreamWaitEvent(s, c->done, 0));
+    int rc = ensure_deep_cap(c, nseg * seg_cap, s);
+    if (rc) return rc;
     /* counters: deep2 (err is sticky until ss_ctx_check) */
     HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
@@ -320,15 +364,20 @@ extern "C" int ss_kernel_time_log(ss_ctx_t *c, double *ms, int cap)
     return ss_kernel_time_log_k(c, SS_KT_MAIN, ms, cap);
 }
 
+/* waits for this context's own work (its latest launch, its stream), not
+ * for other contexts' or the caller's other work on the device */
 extern "C" int ss_ctx_check(ss_ctx_t *c)
 {
     uint32_t err = 0;
     if (!c) return SS_E_INVAL;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(&err, c->d_counters + 2, sizeof(err), hipMemcpyDeviceToHost));
+    hipStream_t hs = c->hstream;
+    if (c->launched) HIPCHK(hipStreamWaitEvent(hs, c->done, 0));
+    HIPCHK(hipMemcpyAsync(&err, c->d_counters + 2, sizeof(err), hipMemcpyDeviceToHost, hs));
+    HIPCHK(hipStreamSynchronize(hs));
     if (err) {
-        HIPCHK(hipMemset(c->d_counters + 2, 0, sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(c->d_counters + 2, 0, sizeof(uint32_t), hs));
+        HIPCHK(hipStreamSynchronize(hs));
         return (err & SS_KERR_MALFORMED) ? SS_E_INVAL : SS_E_CAPACITY;
     }
     return SS_OK;
@@ -337,31 +386,28 @@ extern "C" int ss_ctx_check(ss_ctx_t *c)
 /* ---------------------------------------------------------- host path ---- */
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+/* the host path's staging areas; the previous host call has completed (it
+ * synchronizes its stream), so the old areas are free to go */
 static int ensure_stage(ss_ctx_t *c, size_t bytes)
 {
     if (bytes <= c->h_stage_sz && bytes <= c->d_stage_sz) return SS_OK;
     size_t sz = std::max(bytes, (size_t)1 << 20);
     sz += sz / 4;
-    if (c->h_stage) { hipHostFree(c->h_stage); c->h_stage = nullptr; c->h_stage_sz = 0; }
-    if (c->d_stage) { hipFree(c->d_stage); c->d_stage = nullptr; c->d_stage_sz = 0; }
-    if (hipHostMalloc(&c->h_stage, sz, hipHostMallocDefault) != hipSuccess) return SS_E_NOMEM;
+    HIPCHK(hipStreamSynchronize(c->hstream));
+    pinned_free(c->h_stage);
+    c->h_stage_sz = 0;
+    dev_free(c->d_stage, c->hstream);
+    c->d_stage_sz = 0;
+    if (!(c->h_stage = pinned_alloc(sz))) return SS_E_NOMEM;
     c->h_stage_sz = sz;
-    if (hipMalloc(&c->d_stage, sz) != hipSuccess) return SS_E_NOMEM;
+    if (dev_alloc(&c->d_stage, sz, c->hstream)) return SS_E_NOMEM;
     c->d_stage_sz = sz;
     return SS_OK;
 }
 
-extern "C" void *ss_host_alloc(size_t bytes)
-{
-    void *p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
-    return p;
-}
+extern "C" void *ss_host_alloc(size_t bytes) { return pinned_alloc(bytes); }
 
-extern "C" void ss_host_free(void *p)
-{
-    if (p) hipHostFree(p);
-}
+extern "C" void ss_host_free(void *p) { pinned_free(p); }
 
 /* is [p, p + n) page-locked host memory the device can read directly? */
 /* Pageable input -> pinned staging -> device, in pieces: each piece is copied
@@ -495,17 +541,17 @@ extern "C" int ss_synth_batch_device(ss_ctx_t *c, const ss_synth_t *s, uint64_t 
     int rc = ss_synth_prepare(s, &k, cdf.data(), cdf.data() + SS_SYNTH_MAXCDF);
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemcpy(c->d_cdf, cdf.data(), cdf.size() * 4, hipMemcpyHostToDevice));
+    hipStream_t st = c->hstream;
+    HIPCHK(hipMemcpyAsync(c->d_cdf, cdf.data(), cdf.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));        /* cdf is a local vector */
     k.cdf_tumor = c->d_cdf;
     k.cdf_normal = c->d_cdf + SS_SYNTH_MAXCDF;
-    hipStream_t st = c->hstream;
     if (!rt || !rn) {
         /* pass 1: depths -> exclusive scans -> offsets */
         if (c->depth_tmp_n < 2 * (n + 1)) {
-            if (c->d_depth_tmp) hipFree(c->d_depth_tmp);
-            c->d_depth_tmp = nullptr;
+            dev_free(*(void **)&c->d_depth_tmp, st);
             c->depth_tmp_n = 0;
-            if (dev_alloc((void **)&c->d_depth_tmp, 2 * (n + 1) * 4)) return SS_E_NOMEM;
+            if (dev_alloc((void **)&c->d_depth_tmp, 2 * (n + 1) * 4, st)) return SS_E_NOMEM;
             c->depth_tmp_n = 2 * (n + 1);
         }
         uint32_t *dt = c->d_depth_tmp, *dn = c->d_depth_tmp + (n + 1);
@@ -514,10 +560,9 @@ extern "C" int ss_synth_batch_device(ss_ctx_t *c, const ss_synth_t *s, uint64_t 
         size_t need = 0;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, dt, off_t, (int)(n + 1), st));
         if (need > c->scan_tmp_sz) {
-            if (c->d_scan_tmp) hipFree(c->d_scan_tmp);
-            c->d_scan_tmp = nullptr;
+            dev_free(c->d_scan_tmp, st);
             c->scan_tmp_sz = 0;
-            if (dev_alloc(&c->d_scan_tmp, need)) return SS_E_NOMEM;
+            if (dev_alloc(&c->d_scan_tmp, need, st)) return SS_E_NOMEM;
             c->scan_tmp_sz = need;
         }
         size_t sz = c->scan_tmp_sz;

@@ -1128,7 +1128,10 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
 }
 
 /* lanes 0..16: off_t[s..s+16], 17..32: ref[s..s+15], 33..49: off_n[s..s+16],
- * 50, 51: off_t[n_sites], off_n[n_sites] (the batch's read counts) */
+ * 50, 51: off_t[n_sites], off_n[n_sites] (the batch's read counts), 52: set by
+ * begin_block when the block has an offset past the end (every site of the
+ * block then goes to the deep lists, whose kernels test each site's own
+ * offsets and score a malformed one -2) */
 __device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint32_t s)
 {
     /* The block's bases are wave-uniform (scalar registers); the lane offset is
@@ -1191,7 +1194,8 @@ __device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
     const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n0, 0x130, 0xf, 0xf, false);
     const uint32_t sz = lane < nsite ? (t1 - desc) + (n1 - n0) : 0u;
     BlockScan r;
-    r.deep = __ballot(lane < nsite && off_packed(desc, t1, n0, n1));
+    const bool alldeep = rl(desc, 52u) != 0u;
+    r.deep = __ballot(lane < nsite && (alldeep || off_packed(desc, t1, n0, n1)));
     int x = (int)sz;
     x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);    /* row_shr:1 */
     x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);    /* row_shr:2 */
@@ -1201,28 +1205,34 @@ __device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
     return r;
 }
 
-/* A block becomes current: its offsets are clamped to the batch's read
- * count (descriptor lanes 50 / 51 hold off_t[n], off_n[n]; an offset past it
- * can only come with a decreasing one later, so the batch is flagged
- * malformed, and no load ever leaves the reads), then every site too deep for
- * the packed sort is handed to the wide kernel: one list push per block. */
+/* A block becomes current.  An offset past the batch's read count
+ * (descriptor lanes 50 / 51 hold off_t[n], off_n[n]) flags the batch
+ * malformed and sends the WHOLE block to the deep lists (descriptor lane 52):
+ * the wide and deep kernels test each site's own offsets, so a site that
+ * runs past the end scores -2 like any other malformed site, and no site of
+ * the block is scored on clamped, foreign reads.  The offsets are clamped as
+ * well, so no load of this kernel ever leaves the reads.  Then every site too
+ * deep for the packed sort is handed to the wide kernel: one list push per
+ * block. */
 __device__ __forceinline__ void begin_block(const ss_score_args &a, uint32_t &desc, uint32_t nsite,
                                             uint32_t sblk, uint32_t *seg, uint32_t &ndeep)
 {
     const uint32_t lane = lane_id();
+    bool alldeep = false;
     {
         const uint32_t end = lane < 17u ? rl(desc, 50u) : rl(desc, 51u);
         const bool off_lane = lane < 17u || (lane >= 33u && lane < 50u);
         const bool past = off_lane && desc > end;
         if (__ballot(past)) {
             if (lane == 0) atomicOr(a.err, SS_KERR_MALFORMED);
-            desc = past ? end : desc;
+            desc = past ? end : (lane == 52u ? 1u : desc);
+            alldeep = true;
         }
     }
     const int i = (int)(lane & 15u);
     const uint32_t t0 = (uint32_t)__shfl((int)desc, i), t1 = (uint32_t)__shfl((int)desc, i + 1);
     const uint32_t n0 = (uint32_t)__shfl((int)desc, 33 + i), n1 = (uint32_t)__shfl((int)desc, 34 + i);
-    const bool deep = lane < nsite && off_packed(t0, t1, n0, n1);
+    const bool deep = lane < nsite && (alldeep || off_packed(t0, t1, n0, n1));
     const uint64_t mask = __ballot(deep);
     if (mask == 0) return;
     if (deep) {

@@ -22,9 +22,11 @@
  * later context with the same table parameters shares it) and written to a
  * disk cache keyed by the table parameters AND the machine (CPU vendor /
  * family / model / stepping, glibc version): the tables are CPU-dependent, so
- * a blob is only ever reused on the kind of host that built it.  A blob is
- * verified against the FNV-1a hashes in its header before use; a corrupt or
- * mismatching blob is ignored and replaced.  SS_TABLE_CACHE=<dir> chooses the
+ * a blob is only ever reused on the kind of host that built it.  The key also
+ * holds the builder's identity (SS_TABLE_BUILDER), so a blob from another
+ * builder version is never picked up.  A blob is verified before use: the
+ * FNV-1a hashes of its payload are recomputed and must equal the header's; a
+ * corrupt or mismatching blob is ignored and replaced.  SS_TABLE_CACHE=<dir> chooses the
  * directory (default $XDG_CACHE_HOME/sniper_amd or ~/.cache/sniper_amd),
  * SS_TABLE_CACHE=off disables the disk cache.
  */
@@ -295,12 +297,16 @@ static int g_warned_unpinned;
 
 #define SS_COEF_N ((size_t)64 << 16)
 #define SS_LHET_N ((size_t)65536)
-#define SS_BLOB_MAGIC 0x3130424154535353ull   /* "SSSTAB01" */
+#define SS_BLOB_MAGIC 0x3230424154535353ull   /* "SSSTAB02" */
+/* Identity of the table builder: a blob written by another version of
+ * build_coef / build_lhet / build flags must never be reused.  Bump the
+ * version whenever either builder or the host compile flags change; the
+ * string is part of the cache key (key_hash). */
+#define SS_TABLE_BUILDER "ss_tables v3: build_coef/build_lhet x87, gcc -O2 -ffp-contract=off -fno-fast-math"
 
 typedef struct {
     uint64_t magic, key_hash;
-    uint64_t h_fk, h_coef, h_lhet;       /* FNV-1a-64 (the pinning hashes) */
-    uint64_t check;                      /* word-wise checksum of the payload (integrity) */
+    uint64_t h_fk, h_coef, h_lhet;       /* FNV-1a-64 (the pinning hashes), recomputed on load */
     float q_r;
     int32_t q_r_int;
     uint64_t payload;                      /* bytes after the header */
@@ -345,6 +351,7 @@ static uint64_t key_hash(const tab_key_t *k)
     uint64_t h;
     machine_sig(sig, sizeof sig);
     h = ss_fnv1a64(k, sizeof *k) ^ 0x9e3779b97f4a7c15ull;
+    h ^= ss_fnv1a64(SS_TABLE_BUILDER, sizeof SS_TABLE_BUILDER - 1) * 0xff51afd7ed558ccdull;
     return h ^ (ss_fnv1a64(sig, strlen(sig)) * 0x100000001b3ull);
 }
 
@@ -368,22 +375,6 @@ static int blob_path(const tab_key_t *k, char *out, size_t cap)
     return 1;
 }
 
-/* word-wise multiplicative checksum (a few GB/s): detects any changed,
- * missing or moved 8-byte word of a blob */
-static uint64_t blob_check(const tab_entry_t *t)
-{
-    uint64_t h = 0x243f6a8885a308d3ull;
-    const double *parts[3] = {t->fk, t->coef, t->lhet};
-    const size_t lens[3] = {256, SS_COEF_N, SS_LHET_N};
-    int j;
-    for (j = 0; j < 3; ++j) {
-        const uint64_t *w = (const uint64_t *)parts[j];
-        size_t i;
-        for (i = 0; i < lens[j]; ++i) h = (h ^ w[i]) * 0x9e3779b97f4a7c15ull + (uint64_t)i;
-    }
-    return h;
-}
-
 static int blob_load(const tab_key_t *k, tab_entry_t *t)
 {
     char path[4096];
@@ -395,10 +386,13 @@ static int blob_load(const tab_key_t *k, tab_entry_t *t)
         h.payload == sizeof t->fk + (SS_COEF_N + SS_LHET_N) * sizeof(double) &&
         fread(t->fk, sizeof t->fk, 1, f) == 1 && fread(t->coef, sizeof(double), SS_COEF_N, f) == SS_COEF_N &&
         fread(t->lhet, sizeof(double), SS_LHET_N, f) == SS_LHET_N) {
-        ok = blob_check(t) == h.check;                   /* corrupt: rebuild */
-        t->h_fk = h.h_fk;
-        t->h_coef = h.h_coef;
-        t->h_lhet = h.h_lhet;
+        /* the pinning hashes are recomputed from the payload (about 30 ms), never
+         * taken from the header: a corrupt, truncated or foreign blob whose bytes
+         * differ from what its header claims is rebuilt */
+        t->h_fk = ss_fnv1a64(t->fk, sizeof t->fk);
+        t->h_coef = ss_fnv1a64(t->coef, SS_COEF_N * sizeof(double));
+        t->h_lhet = ss_fnv1a64(t->lhet, SS_LHET_N * sizeof(double));
+        ok = t->h_fk == h.h_fk && t->h_coef == h.h_coef && t->h_lhet == h.h_lhet;
         t->q_r = h.q_r;
         t->q_r_int = h.q_r_int;
     }
@@ -433,7 +427,6 @@ static void blob_store(const tab_key_t *k, const tab_entry_t *t)
     h.h_fk = t->h_fk;
     h.h_coef = t->h_coef;
     h.h_lhet = t->h_lhet;
-    h.check = blob_check(t);
     h.q_r = t->q_r;
     h.q_r_int = t->q_r_int;
     h.payload = sizeof t->fk + (SS_COEF_N + SS_LHET_N) * sizeof(double);

@@ -146,7 +146,7 @@ def test_table_cache_reuse_and_corruption(tmp_path):
     assert r2["first"]["source"] == "disk"
     for k in ("fk", "coef", "lhet", "q_r", "pinned"):
         assert r2["first"][k] == r1["first"][k], k
-    assert r2["secs"] < r1["secs"] / 3, (r2["secs"], r1["secs"])
+    assert r2["secs"] < r1["secs"] / 2, (r2["secs"], r1["secs"])
     # corrupt one coef double: detected, rebuilt, the blob rewritten
     raw = bytearray(blobs[0].read_bytes())
     raw[4096 + 1234567] ^= 0x40

@@ -91,6 +91,17 @@ def test_native_cli_usage_and_errors(tmp_path):
     assert p.returncode == 0 and p.stdout.startswith("Somatic Sniper version")
 
 
+@need_native
+@pytest.mark.parametrize("devs,msg", [("0,x", "bad entry"), ("0,,1", "bad entry"), ("-1", "bad entry"),
+                                      ("1,1", "listed twice"), (",".join(map(str, range(17))), "more than 16")])
+def test_ss_devices_rejects_bad_lists(datasets, devs, msg):
+    """SS_DEVICES must be a list of distinct GPU indices: a typo fails loudly
+    before any GPU work instead of quietly sharing or renumbering devices."""
+    d, fa, t, n = datasets[0]
+    p = _run([NATIVE, "-f", fa, t, n, "devs.out"], d, {"SS_DEVICES": devs})
+    assert p.returncode == 1 and "SS_DEVICES" in p.stderr and msg in p.stderr, p.stderr
+
+
 @pytest.mark.gpu
 @need_native
 def test_native_integration_expected_vcf(datasets):
@@ -178,7 +189,8 @@ def test_multi_scorer_output_identical(datasets):
             args = ["-F", fmt, "-Q", "0", "-f", fa, t, n]
             pr = _run([REF_CLI] + args + ["ref_ms.out"], d)
             p1 = _run([NATIVE] + args + ["one_ms.out"], d, {"SS_BATCH": "97"})
-            p3 = _run([NATIVE] + args + ["three_ms.out"], d, {"SS_BATCH": "97", "SS_DEVICES": "0,0,0"})
+            p3 = _run([NATIVE] + args + ["three_ms.out"], d, {"SS_BATCH": "97", "SS_DEVICES": "0,0,0",
+                                                                   "SS_DEVICES_SHARED": "1"})
             assert pr.returncode == p1.returncode == p3.returncode == 0, (p1.stderr, p3.stderr)
             strip = lambda s: "".join(l for l in s.splitlines(True) if not l.startswith("##fileDate"))
             ref = strip(open(os.path.join(d, "ref_ms.out")).read())

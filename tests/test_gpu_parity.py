@@ -70,16 +70,19 @@ def test_synthetic_parity(pkg, oracle, lt, ln, kw, opts):
                                                 (300, 300, 0, 300, 0.0), (500, 500, 0, 200, 0.0),
                                                 (700, 700, 1, 60, 0.0), (600, 500, 0, 120, 0.0),
                                                 (500, 500, 0, 300, 0.0005)])
-def test_deep_parity(pkg, oracle, ctx, lt, ln, fixed, n, wild):
+@pytest.mark.parametrize("opts", OPTSETS)
+def test_deep_parity(pkg, oracle, lt, ln, fixed, n, wild, opts):
     """Sites beyond the main kernel's 512 sort slots -> wide kernel (and the
     deep kernel past 2048); > 255 reads per class saturates w, > 255 total
     rescales c (Appendix A.4).  The wide kernel's 8-bit fold records hold
     q < 64, so a site with a read of minq >= 64 (wild qualities: baseQ / mapQ
     up to 255) is scored by the deep kernel instead: wild = 0.05 sends every
-    wide site there, 0 none, 5e-4 about a quarter (mixed routing)."""
+    wide site there, 0 none, 5e-4 about a quarter (mixed routing).  Every
+    option set: -T/-N/-r change the fk / coef / lhet tables the wide and deep
+    folds and likelihoods read, -J/-p/-L/-G/-Q the decision."""
     kw = dict(EXOTIC, p_wild_qual=wild)
     batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=fixed, **kw), 0, n)
-    assert_parity(pkg, oracle, batch, ctx=ctx)
+    assert_parity(pkg, oracle, batch, opts)
 
 
 @pytest.mark.parametrize("lt,ln,fixed,n,wild", [(1200, 1000, 0, 60, 0.0), (1500, 600, 1, 30, 0.0),
@@ -88,7 +91,8 @@ def test_deep_parity(pkg, oracle, ctx, lt, ln, fixed, n, wild):
                                                 (700, 480, 1, 40, 0.0), (480, 1050, 1, 40, 0.0),
                                                 (1000, 300, 1, 40, 0.0), (560, 470, 0, 200, 0.0),
                                                 (560, 470, 0, 120, 0.0005)])
-def test_wide_sample_units_parity(pkg, oracle, ctx, lt, ln, fixed, n, wild):
+@pytest.mark.parametrize("opts", OPTSETS)
+def test_wide_sample_units_parity(pkg, oracle, lt, ln, fixed, n, wild, opts):
     """Sites past 2048 sort slots whose samples have at most 2048 reads each:
     the wide kernel sorts each sample in a network of its own (sort units),
     K = 8 or 16 per sample; a sample beyond 2048 (2100/100) and sites with
@@ -97,14 +101,15 @@ def test_wide_sample_units_parity(pkg, oracle, ctx, lt, ln, fixed, n, wild):
     560/470) are units too: K = 4 for the small sample, 8 for the other."""
     kw = dict(EXOTIC, p_wild_qual=wild)
     batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=fixed, **kw), 3, n)
-    assert_parity(pkg, oracle, batch, ctx=ctx)
+    assert_parity(pkg, oracle, batch, opts)
 
 
-def test_kernel_routing_mix(pkg, oracle, ctx):
+@pytest.mark.parametrize("opts", OPTSETS)
+def test_kernel_routing_mix(pkg, oracle, opts):
     """One batch whose sites take every route: main kernel (<= 512 sort slots),
     wide kernel (<= 2048), and the deep kernel via the wide kernel's overflow
     list (histogram fold, any depth), interleaved so each kernel sees
-    non-contiguous site indices."""
+    non-contiguous site indices; under every option set."""
     parts = [pkg.synth_batch_host(pkg.Synth.default(lt, ln, fixed_depth=1, **EXOTIC), 7 * k, n)
              for k, (lt, ln, n) in enumerate([(60, 30, 40), (600, 500, 12), (1500, 1200, 6), (4200, 300, 3),
                                               (30, 2, 40), (900, 900, 6)])]
@@ -113,8 +118,9 @@ def test_kernel_routing_mix(pkg, oracle, ctx):
         for b in parts:
             if i < b.n_sites:
                 sites.append(b.site(i))
-    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), ctx=ctx)
-    ctx.check()
+    with pkg.Context(params_from_opts(pkg, opts), device=0) as c:
+        assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), opts, ctx=c)
+        c.check()
 
 
 def test_pinned_host_batch(pkg, oracle, ctx):
@@ -178,10 +184,10 @@ def test_malformed_offsets_reported(pkg, oracle, ctx, case):
         minus2 = [202]
     elif case == "past_end":
         ot[100] = ot[n] + 1000                        # site 99 runs past the end, site 100 decreases
-        minus2 = [100]
+        minus2 = [99, 100]
     else:
         ot[50] = ot[51] = ot[n] + 77
-        minus2 = [51]
+        minus2 = [49, 50, 51]                         # 49 and 50 run past the end, 51 decreases
     bad = pkg.Batch(good.ref, ot, on, good.reads_tumor, good.reads_normal)
     with pytest.raises(pkg.SniperError) as ei:
         ctx.score_batch(bad)
@@ -216,7 +222,8 @@ def test_many_deep_sites(pkg, oracle, ctx):
     ctx.check()
 
 
-def test_deep_windows_full_quality_range(pkg, oracle, ctx):
+@pytest.mark.parametrize("opts", OPTSETS)
+def test_deep_windows_full_quality_range(pkg, oracle, opts):
     """Deep sites whose reads span mapQ and baseQ 0..255 (every bin of the
     deep kernel's 1136 per group is reachable), both strands, every nt16 code:
     the histogram is built and folded in several LDS windows from the top
@@ -231,8 +238,9 @@ def test_deep_windows_full_quality_range(pkg, oracle, ctx):
         sites.append(("ACGT"[k % 4], mk(nt_), mk(nn_)))
     lowq = [pkg.pack_read(60, int(5 + i % 20), 1 + (i % 3), i & 1) for i in range(2400)]
     sites.append(("A", lowq + [pkg.pack_read(250, 240, 8, 1)], lowq[:900]))
-    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), ctx=ctx)
-    ctx.check()
+    with pkg.Context(params_from_opts(pkg, opts), device=0) as c:
+        assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), opts, ctx=c)
+        c.check()
 
 
 def test_giant_parity(pkg, oracle, ctx):
@@ -290,7 +298,7 @@ def quirk_sites(pkg):
     return s
 
 
-@pytest.mark.parametrize("opts", [[], ["-J"], ["-Q", "0", "-L", "-G"], ["-p"]])
+@pytest.mark.parametrize("opts", OPTSETS)
 def test_quirk_parity(pkg, oracle, opts):
     batch = pkg.Batch.from_sites(quirk_sites(pkg))
     score, _ = assert_parity(pkg, oracle, batch, opts)
@@ -367,14 +375,16 @@ def test_gpu_matches_real_reference_on_this_host(pkg, tmp_path):
         assert len(calls) == txt.count("\n")
 
 
-@pytest.mark.parametrize("lt,ln,n", [(60, 30, 1 << 22), (30, 30, 1 << 22), (100, 60, 1 << 21),
-                                     (500, 500, 1 << 16)])
-def test_full_size_batch_vs_real_reference(pkg, ctx, tmp_path, lt, ln, n):
+@pytest.mark.parametrize("lt,ln,n,opts", [(60, 30, 1 << 22, []), (30, 30, 1 << 22, []), (100, 60, 1 << 21, []),
+                                          (500, 500, 1 << 16, []), (500, 500, 1 << 16, ["-J"]),
+                                          (500, 500, 1 << 16, ["-T", "0.9", "-N", "3", "-r", "0.01"])])
+def test_full_size_batch_vs_real_reference(pkg, tmp_path, lt, ln, n, opts):
     """Large batches of the BASELINE depth configurations (C4 60x/30x -- the
     headline --, C2, C3, C5; default seed, shard 0), generated and scored in
     HBM, against the compiled reference's glf_somatic on the same sites run on
     this host by 16 processes (oracle/_ref/ref_harness synth --first): every
-    site's return value bit-exact."""
+    site's return value bit-exact.  C5 (the wide kernel's depth) also under
+    -J and under -T/-N/-r (other fk / coef / lhet tables)."""
     import os
     import subprocess
     torch = pytest.importorskip("torch")
@@ -382,18 +392,20 @@ def test_full_size_batch_vs_real_reference(pkg, ctx, tmp_path, lt, ln, n):
     if not os.path.exists(ob.REF_HARNESS):
         pytest.skip("reference harness not built")
     procs = 16
-    d = ctx.synth_device(pkg.Synth.default(lt, ln), 0, n)
-    score = torch.empty(n, dtype=torch.int32, device=d["ref"].device)
-    ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
-                     score=score)
-    ctx.check()
-    gpu = score.cpu().numpy()
+    with pkg.Context(params_from_opts(pkg, opts), device=0) as ctx:
+        d = ctx.synth_device(pkg.Synth.default(lt, ln), 0, n)
+        score = torch.empty(n, dtype=torch.int32, device=d["ref"].device)
+        ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                         score=score)
+        ctx.check()
+        gpu = score.cpu().numpy()
+        del d
     step = n // procs
     runs = []
     for k in range(procs):
         out = str(tmp_path / f"s{k}.bin")
         runs.append((out, subprocess.Popen([ob.REF_HARNESS, "synth", str(lt), str(ln), str(step), "--first",
-                                            str(k * step), "--scores", out],
+                                            str(k * step), "--scores", out] + list(opts),
                                            stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)))
     for out, p in runs:
         assert p.wait(timeout=100) == 0, p.stderr.read()[-500:]

@@ -195,3 +195,65 @@ def test_one_context_two_streams(pkg):
         assert torch.equal(o1, r1) and torch.equal(o2, r2)
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_contexts_do_not_wait_for_each_other(pkg):
+    """Contexts are independent (include/sniper_amd.h): with context A's long
+    queue of device-path launches (500x/500x sites, the wide kernel) still
+    running on its stream, context B's synchronous ss_score_batch_host on 4k
+    sites returns -- B waits for its own work only, never for the device.
+    Both results are bit-exact (A against a lone launch of the same batch and
+    the oracle on a prefix, B against the oracle)."""
+    import time
+    import torch
+    from oracle import binding as ob
+    dev = torch.device("cuda", 0)
+    ca = pkg.Context(pkg.Params.default(), device=0)
+    cb = pkg.Context(pkg.Params.default(), device=0)
+    try:
+        n_a = 1 << 18
+        syn_a = pkg.Synth.default(500, 500, p_somatic=0.02)
+        d = ca.synth_device(syn_a, 0, n_a, device=dev)
+        bb = pkg.synth_batch_host(pkg.Synth.default(60, 30, p_somatic=0.02, p_germline=0.02), 0, 4096)
+        warm = cb.score_batch(bb)[0]                 # B's staging and lists exist before A starts
+        sa = torch.cuda.Stream(dev)
+        lone = torch.empty(n_a, dtype=torch.int32, device=dev)
+        ca.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                        score=lone, stream=sa)
+        sa.synchronize()
+        t0 = time.perf_counter()
+        ca.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                        score=lone, stream=sa)
+        sa.synchronize()
+        one = time.perf_counter() - t0
+        n_launch = max(8, int(0.4 / max(one, 1e-4)))     # about 0.4 s of A's work queued
+        outs = [torch.empty(n_a, dtype=torch.int32, device=dev) for _ in range(2)]
+        for i in range(n_launch):
+            ca.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                            score=outs[i % 2], stream=sa)
+        a_done = torch.cuda.Event()
+        a_done.record(sa)
+        t_q = time.perf_counter()
+        got_b = cb.score_batch(bb)[0]
+        t_b = time.perf_counter() - t_q
+        a_busy = not a_done.query()
+        a_done.synchronize()
+        t_a = time.perf_counter() - t_q
+        assert a_busy, f"B's host call returned only after A's queue drained (B {t_b:.3f} s, A {t_a:.3f} s)"
+        assert t_b < 0.5 * t_a, (t_b, t_a)
+        o = ob.Oracle()
+        ob_score = o.score_batch(bb.ref, bb.off_tumor, bb.off_normal, bb.reads_tumor, bb.reads_normal,
+                                 want_glf=False)[0]
+        assert (got_b == ob_score).all() and (warm == ob_score).all()
+        ref_a = lone.cpu().numpy()
+        for x in outs:
+            assert (x.cpu().numpy() == ref_a).all()
+        ha = pkg.synth_batch_host(syn_a, 0, 2000)
+        assert (ref_a[:2000] == o.score_batch(ha.ref, ha.off_tumor, ha.off_normal, ha.reads_tumor,
+                                              ha.reads_normal, want_glf=False)[0]).all()
+        ca.check()
+        cb.check()
+    finally:
+        ca.close()
+        cb.close()
