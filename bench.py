@@ -1,26 +1,34 @@
 #!/usr/bin/env python3
 """bench.py -- pileup sites/sec of the MI355X somatic scorer (BASELINE.json metric).
 
-One STEP = one pass of the scoring path (ss_score_batch_device: main + wide +
-deep kernels) over one HBM-resident batch of synthetic 60xT/30xN pileup sites
-(Poisson depths).  Inputs are generated on the device before
-timing; the timed region contains only scoring.
+Workload c4 (default; BASELINE.json configs[3]): the 24 GRCh38 primary contigs
+as a synthetic genome (one pileup site per position, 60xT/30xN Poisson depths,
+SURVEY.md 8(d)), divided by --c4-scale (16: 1.93e8 sites, which fits one
+GPU's HBM at N=1), contigs assigned to ranks by sharding.shard_contigs.  Sites
+are keyed by (contig, position): synth shard = contig index.  One STEP = every
+rank scores its share of the genome once (ss_score_batch_device per contig:
+main + wide + deep kernels) -- total work fixed, strong scaling.  Workload
+shard: --sites sites per rank per step (weak scaling; the C2/C3/C5 depth
+runs).  Inputs are generated on the device before timing; the timed region
+contains only scoring.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL backend only for the
 barrier and the max-over-ranks timing reduction).  Each rank scores its own
-genome shard (synth shard = rank) -- no collective on the data path, weak
-scaling.  value = sites scored by all ranks / max rank time.  Launched either
+contigs -- no collective on the data path.  value = sites scored by all ranks
+/ max rank time.  A secondary weak-scaling line (an equal synthetic shard per
+GPU) is reported as "weak_scaling".  Launched either
 by torch.distributed.run (RANK/WORLD_SIZE/LOCAL_RANK in the environment) or
 directly as ``bench.py --gpus N``: the parent then starts N fresh rank
 processes itself before anything touches the GPU, stays GPU-free, and relays
 rank 0's line.
 
-Extra fields: "roofline" (main kernel, HIP events over the timed region,
-algorithmic bytes 4 B/read + 16 B/site), "cpu_baseline" (the real reference
-glf_somatic compiled from source, oracle/_ref/ref_harness, 1 core, rank 0 at
-N=1 only, on a bounded sample of the same synthetic workload, also used as a
-parity spot check) and "cpu_baseline_all_cores" (the same on every core we may
-use, one process per core).
+Extra fields: "roofline" (the kernel with the most time, HIP events over the
+timed region's launches, algorithmic bytes 4 B/read + 16 B/site per launch),
+"cpu_baseline" (the real reference glf_somatic compiled from source,
+oracle/_ref/ref_harness, 1 core, rank 0 at N=1 only, on a bounded sample of
+the same synthetic workload -- about the same CPU time at any depth --, also
+used as a parity spot check) and "cpu_baseline_all_cores" (the same on every
+core we may use, one process per core).
 """
 from __future__ import annotations
 
@@ -54,8 +62,9 @@ def cpu_baseline(lt, ln, sample, seed, gpu_scores_prefix):
         kind, value = "reference", r["sites_per_s"]
         cpu_scores = np.fromfile(scores_path, np.int32)
         os.unlink(scores_path)
-        desc = (f"{sample} synthetic sites ({lt}xT/{ln}xN, shard 0, first sites of step batch 0), "
-                f"reference glf_somatic only (pileups prebuilt, BAM decode excluded), 1 thread")
+        desc = (f"{sample} synthetic sites ({lt}xT/{ln}xN, synth shard 0 from site 0: the first positions of "
+                f"contig 0 of the c4 workload / of rank 0's batch 0 of the shard workload), reference glf_somatic "
+                f"only (pileups prebuilt, BAM decode excluded), 1 thread")
     else:
         from __graft_entry__ import load_package
         from oracle import binding as ob
@@ -178,17 +187,22 @@ PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
 
 
 def pmc_child(args):
-    """--pmc-child: the bench's batch 0 of shard 0 scored a few times, nothing
-    else (run under rocprofv3 by live_counters)."""
+    """--pmc-child: the bench's own launches (rank 0 of a 1-GPU run: every c4
+    contig, or the shard workload's batch 0), scored --pmc-launches passes,
+    nothing else (run under rocprofv3 by live_counters)."""
     import torch
     from __graft_entry__ import load_package
     pkg = load_package()
     dev = torch.device("cuda", 0)
     ctx = pkg.Context(pkg.Params.default(), device=0)
-    d = ctx.synth_device(pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=0), 0, args.sites, device=dev)
-    score = torch.empty(args.sites, dtype=torch.int32, device=dev)
+    if args.workload == "shard":
+        args.batches = 1
+    batches = make_batches(ctx, pkg, args, 0, 1, dev)
+    scores = [torch.empty(max(1, d["n_sites"]), dtype=torch.int32, device=dev) for d in batches]
     for _ in range(args.pmc_launches):
-        ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"], score=score)
+        for d, sc in zip(batches, scores):
+            ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                             score=sc)
     torch.cuda.synchronize(dev)
     ctx.check()
     ctx.close()
@@ -213,7 +227,8 @@ def live_counters(args, kernel="ss_score_main"):
         out = tempfile.mkdtemp(prefix="ss_pmc_", dir="/tmp")
         try:
             cmd = [exe, "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "run", "--",
-                   sys.executable, os.path.abspath(__file__), "--pmc-child", "--sites", str(args.sites),
+                   sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
+                   "--c4-scale", str(args.c4_scale), "--chunk", str(args.chunk), "--sites", str(args.sites),
                    "--lt", str(args.lt), "--ln", str(args.ln), "--seed", str(args.seed),
                    "--pmc-launches", str(args.pmc_launches)]
             # own process group: a pass that overruns is killed with its python child
@@ -240,15 +255,27 @@ def live_counters(args, kernel="ss_score_main"):
                     if re.search(re.escape(kernel) + r"[<(]", row["Kernel_Name"]):
                         d = per.setdefault(int(row["Dispatch_Id"]), {})
                         d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
-            ds = sorted(per)[1:] or sorted(per)
+            # one pass = one launch per batch; the first pass (cold tables) is dropped
+            n_pass = len(per) // max(1, args.pmc_launches)
+            ds = sorted(per)[n_pass:] or sorted(per)
             for c in counters:
                 vals[c] = float(np.mean([per[k].get(c, 0.0) for k in ds]))
+            vals["_sites_per_launch"] = sites_per_launch(args)
         except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
             print(f"bench: PMC pass {counters} failed: {e}", file=sys.stderr)
             return None
         finally:
             shutil.rmtree(out, ignore_errors=True)
     return vals
+
+
+def sites_per_launch(args) -> float:
+    """Mean sites per launch of the PMC child's workload (rank 0 of one GPU)."""
+    if args.workload == "shard":
+        return float(args.sites)
+    _, sizes, _ = c4_layout(args.c4_scale, 1)
+    n = [min(args.chunk, s - f) for s in sizes for f in range(0, s, args.chunk)]
+    return float(np.mean(n))
 
 
 def cpu_model() -> str:
@@ -262,17 +289,72 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def depth_scaled(n: int, lt: float, ln: float) -> int:
+    """A CPU-baseline sample of about the same CPU time at any depth: the
+    reference's glf_somatic costs about linearly in the reads per site, and n
+    is the sample size at 60xT/30xN (89.1 non-deleted reads per site)."""
+    return max(10_000, int(n * 89.1 / max(1.0, lt + ln)))
+
+
+def c4_layout(scale: int, world: int):
+    """Config C4 (BASELINE.json configs[3]): the 24 GRCh38 primary contigs, one
+    synthetic site per position, the genome divided by `scale`; contigs are
+    assigned to ranks by sharding.shard_contigs.  Returns (names, sites per
+    contig, plan)."""
+    import importlib
+    sh = importlib.import_module("somatic_sniper_amd.sharding")
+    names = [n for n, _ in sh.GRCH38_PRIMARY]
+    sizes = [-(-length // scale) for _, length in sh.GRCH38_PRIMARY]
+    return names, sizes, sh.shard_contigs(sizes, world)
+
+
+def make_batches(ctx, pkg, args, rank, world, dev):
+    """The rank's HBM-resident synthetic input, generated on the device.
+    c4: every contig of the rank's plan, keyed by (contig, position) -- synth
+    shard = contig index, site = position --, one launch per contig (split into
+    launches of at most --chunk sites).  shard: --batches batches of --sites
+    sites of synth shard = rank."""
+    out = []
+    if args.workload == "c4":
+        names, sizes, plan = c4_layout(args.c4_scale, world)
+        for tid in plan[rank]:
+            syn = pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=tid)
+            for first in range(0, sizes[tid], args.chunk):
+                n = min(args.chunk, sizes[tid] - first)
+                d = ctx.synth_device(syn, first, n, device=dev)
+                d.update(tid=tid, first=first)
+                out.append(d)
+    else:
+        S = args.sites
+        for b in range(args.batches):
+            syn = pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=rank)
+            d = ctx.synth_device(syn, b * S, S, device=dev)
+            d.update(tid=rank, first=b * S)
+            out.append(d)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--sites", type=int, default=1 << 26, help="sites per batch (per step, per GPU)")
-    ap.add_argument("--batches", type=int, default=2, help="distinct resident batches cycled per rank")
+    ap.add_argument("--workload", choices=("c4", "shard"), default="c4",
+                    help="c4: GRCh38 contig-sharded genome (BASELINE config C4; strong scaling, total work fixed); "
+                         "shard: --sites synthetic sites per rank (weak scaling; the C2/C3/C5 depth runs)")
+    ap.add_argument("--c4-scale", type=int, default=16,
+                    help="C4 genome sites divided by this (3.09e9 / 16 = 1.93e8 sites: fits one GPU at N=1)")
+    ap.add_argument("--chunk", type=int, default=1 << 26, help="c4: most sites per launch")
+    ap.add_argument("--sites", type=int, default=1 << 26, help="shard: sites per batch (per step, per GPU)")
+    ap.add_argument("--batches", type=int, default=2, help="shard: distinct resident batches cycled per rank")
+    ap.add_argument("--weak-sites", type=int, default=1 << 26,
+                    help="c4: sites per GPU of the secondary weak-scaling line (0 = skip it)")
+    ap.add_argument("--weak-steps", type=int, default=10)
     ap.add_argument("--lt", type=float, default=60.0)
     ap.add_argument("--ln", type=float, default=30.0)
     ap.add_argument("--seed", type=int, default=0x5EED5A1DC0FFEE01)
-    ap.add_argument("--cpu-sample", type=int, default=2_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="sites of the 1-core reference baseline (default: 2M at 60x/30x, scaled by depth)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", default="nccl",
                     help="process-group backend for N>1 (nccl = RCCL; gloo rehearses N ranks on one GPU)")
@@ -288,6 +370,8 @@ def main():
         sys.exit(f"bench.py: refusing to time with tuning/diagnostic variables set: {', '.join(bad)}")
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
+    if args.c4_scale < 1 or args.chunk < 1:
+        sys.exit("bench.py: --c4-scale and --chunk must be >= 1")
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
             sys.exit(spawn_ranks(args.gpus))      # parent: no torch, no GPU
@@ -316,35 +400,39 @@ def main():
     torch.cuda.set_device(dev)
 
     from __graft_entry__ import load_package
+    import importlib
     pkg = load_package()
+    sharding = importlib.import_module("somatic_sniper_amd.sharding")
     ctx = pkg.Context(pkg.Params.default(), device=local)
     pinned = pkg.model_check()["pinned"]
 
-    # ---- resident synthetic batches (this rank's shard) ----
-    S = args.sites
-    batches = []
-    for b in range(args.batches):
-        syn = pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=rank)
-        d = ctx.synth_device(syn, b * S, S, device=dev)
-        batches.append(d)
+    # ---- resident synthetic input (this rank's contigs / shard) ----
+    batches = make_batches(ctx, pkg, args, rank, world, dev)
     torch.cuda.synchronize(dev)
-    if max(max(d["n_reads"]) for d in batches) >= 1 << 32:
-        sys.exit("bench.py: a batch holds >= 2^32 reads of one sample (u32 offsets); lower --sites")
+    if batches and max(max(d["n_reads"]) for d in batches) >= 1 << 32:
+        sys.exit("bench.py: a batch holds >= 2^32 reads of one sample (u32 offsets); lower --chunk / --sites")
     reads = [sum(d["n_reads"]) for d in batches]
-    bytes_per_batch = [4 * r + 16 * S for r in reads]
-    score = [torch.empty(S, dtype=torch.int32, device=dev) for _ in batches]
-    cap = max(1024, S // 256)
+    bytes_of = [4 * r + 16 * d["n_sites"] for r, d in zip(reads, batches)]
+    score = [torch.empty(max(1, d["n_sites"]), dtype=torch.int32, device=dev) for d in batches]
+    cap = max(1024, max([d["n_sites"] for d in batches] + [0]) // 256)
     calls = torch.zeros(cap * 28, dtype=torch.uint8, device=dev)
     ncalls = torch.zeros(1, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    c4 = args.workload == "c4"
+    # a step: c4 scores every batch of the rank (its share of the genome, once);
+    # shard scores one batch, cycling through the resident ones
+    per_step = list(range(len(batches))) if c4 else None
+
+    def launch(k):
+        d = batches[k]
+        ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                         score=score[k], calls=calls, calls_cap=cap, n_calls=ncalls, stream=stream)
 
     def step(i):
-        k = i % len(batches)
-        d = batches[k]
-        ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"],
-                         d["reads_normal"], score=score[k], calls=calls, calls_cap=cap,
-                         n_calls=ncalls, stream=stream)
-        return k
+        ks = per_step if c4 else [i % len(batches)]
+        for k in ks:
+            launch(k)
+        return ks
 
     for i in range(args.warmup):
         step(i)
@@ -359,7 +447,7 @@ def main():
     t0 = time.perf_counter()
     used = []
     for i in range(args.steps):
-        used.append(step(i))
+        used.extend(step(i))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -367,19 +455,52 @@ def main():
     ctx.set_kernel_timing(False)
     ctx.check()
     elapsed = t1 - t0
-    # per-kernel HIP-event durations; the roofline is quoted for the dominant one
+    # per-kernel HIP-event durations of the logged launches (the first 4096);
+    # the roofline is quoted for the kernel with the most time
     klog = {k: ctx.kernel_time_log(k) for k in ("main", "wide", "deep")}
+    ksum = {k: float(np.sum(v)) for k, v in klog.items()}
     kmean = {k: float(np.mean(v)) if len(v) else 0.0 for k, v in klog.items()}
-    dom = max(kmean, key=kmean.get)
+    dom = max(ksum, key=ksum.get)
     kms = klog[dom]
-    sites_rank = S * args.steps
-    import importlib
-    sharding = importlib.import_module("somatic_sniper_amd.sharding")
+    logged = used[: len(kms)]
+    sites_step_rank = sum(batches[k]["n_sites"] for k in (per_step if c4 else [0]))
+    sites_rank = sum(batches[k]["n_sites"] for k in used)
     rank_elapsed = elapsed
     elapsed, total_sites, _ = sharding.aggregate(elapsed, sites_rank, world)
     prop = torch.cuda.get_device_properties(dev)
     me = {"rank": rank, "device": local, "pci_bus_id": getattr(prop, "pci_bus_id", None),
-          "ms_per_step": round(rank_elapsed / args.steps * 1e3, 4), "sites": sites_rank}
+          "ms_per_step": round(rank_elapsed / args.steps * 1e3, 4), "sites": sites_rank,
+          "sites_per_step": sites_step_rank, "launches_per_step": len(per_step) if c4 else 1}
+    if c4:
+        names, sizes, plan = c4_layout(args.c4_scale, world)
+        me["contigs"] = [names[t] for t in plan[rank]]
+
+    # ---- secondary weak-scaling line (c4 only): an equal synthetic shard per GPU ----
+    weak = None
+    if c4 and args.weak_sites > 0 and args.weak_steps > 0:
+        wd = ctx.synth_device(pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=1000 + rank), 0,
+                              args.weak_sites, device=dev)
+        wscore = torch.empty(args.weak_sites, dtype=torch.int32, device=dev)
+        wargs = (wd["ref"], wd["off_tumor"], wd["off_normal"], wd["reads_tumor"], wd["reads_normal"])
+        ctx.score_device(*wargs, score=wscore, calls=calls, calls_cap=cap, n_calls=ncalls, stream=stream)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        w0 = time.perf_counter()
+        for _ in range(args.weak_steps):
+            ctx.score_device(*wargs, score=wscore, calls=calls, calls_cap=cap, n_calls=ncalls, stream=stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        w_el, w_sites, w_rate = sharding.aggregate(time.perf_counter() - w0, args.weak_sites * args.weak_steps,
+                                                   world)
+        ctx.check()
+        weak = {"value": round(w_rate, 1), "unit": "sites/s", "scaling": "weak",
+                "sites_per_step_per_gpu": args.weak_sites, "steps": args.weak_steps,
+                "ms_per_step": round(w_el / args.weak_steps * 1e3, 4),
+                "workload": f"synthetic shard per GPU (synth shard 1000 + rank), {args.lt:g}xT/{args.ln:g}xN"}
+        del wd, wscore
+
     if world > 1:
         ranks = [None] * world
         dist.all_gather_object(ranks, me)
@@ -389,8 +510,25 @@ def main():
         print(f"bench: ranks {[(r['rank'], r['device'], r['pci_bus_id']) for r in ranks]}", file=sys.stderr)
 
     avg_kernel_ms = float(np.mean(kms)) if len(kms) else None
-    alg_bytes = float(np.mean([bytes_per_batch[k] for k in used]))
-    achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms else None
+    alg_bytes = float(np.mean([bytes_of[k] for k in logged])) if logged else None
+    achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms and alg_bytes else None
+    mean_reads = float(np.sum(reads)) / max(1, sum(d["n_sites"] for d in batches))
+    if c4:
+        genome_sites = sum(sizes)
+        config = {"workload": f"C4: synthetic GRCh38 (24 primary contigs, one site per position) / {args.c4_scale}, "
+                              f"{args.lt:g}xT/{args.ln:g}xN Poisson depth, contig-sharded",
+                  "genome_sites_per_step": genome_sites, "c4_scale": args.c4_scale,
+                  "sharding": "sharding.shard_contigs (LPT + local search on the contig lengths)",
+                  "plan_imbalance": round(sharding.plan_imbalance(sizes, plan), 5),
+                  "contigs_per_rank": [len(p) for p in plan],
+                  "max_sites_per_launch": args.chunk}
+        assert sum(r["sites_per_step"] for r in ranks) == genome_sites, "a contig scored twice or not at all"
+    else:
+        config = {"workload": f"synthetic shard per GPU, {args.lt:g}xT/{args.ln:g}xN Poisson depth",
+                  "sites_per_step_per_gpu": args.sites, "resident_batches": len(batches)}
+    config.update({"mean_reads_per_site": round(mean_reads, 2),
+                   "parallelism": f"{'contig' if c4 else 'region'}-sharded x{world}, no collectives",
+                   "model_tables_pinned": pinned, "library": library_id(pkg)})
     result = {
         "metric": METRIC,
         "value": round(total_sites / elapsed, 1),
@@ -400,15 +538,11 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c4 else "weak",
         "vs_baseline": None,
         "dtype": "f32+f64 (u32 packed reads)",
         "data": "synthetic (device-generated counter-based pileups, Poisson depth)",
-        "config": {"workload": f"synthetic WGS shard per GPU, {args.lt:g}xT/{args.ln:g}xN Poisson depth",
-                   "sites_per_step_per_gpu": S, "resident_batches": len(batches),
-                   "mean_reads_per_site": round(float(np.mean(reads)) / S, 2),
-                   "parallelism": f"region-sharded x{world}, no collectives",
-                   "model_tables_pinned": pinned, "library": library_id(pkg)},
+        "config": config,
         "ranks": ranks,
         "roofline": {
             "bound": "hbm",
@@ -421,8 +555,23 @@ def main():
             "algorithmic_bytes_per_launch": alg_bytes,
             "avg_kernel_ms": round(avg_kernel_ms, 4) if avg_kernel_ms else None,
             "avg_ms_by_kernel": {k: round(v, 4) for k, v in kmean.items()},
+            "launches_timed": len(kms),
         },
     }
+    if weak:
+        result["weak_scaling"] = weak
+    # GPU scores the CPU baseline is checked against: the first sites of synth
+    # shard 0 (c4: contig 0, position 0 on; shard: rank 0's batch 0)
+    sample = depth_scaled(2_000_000, args.lt, args.ln) if args.cpu_sample is None else args.cpu_sample
+    pre = None
+    for k, d in enumerate(batches):
+        if d["tid"] == 0 and d["first"] == 0:
+            sample = min(sample, d["n_sites"])
+            pre = score[k][:sample].cpu().numpy()
+    # free the resident batches before the counter passes start their own copy
+    del batches, score
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_pmc:
         # live counters of the dominant kernel on this same workload (separate
         # rocprofv3 passes after the timed region; MI355X_MICROARCH.md: FETCH_SIZE
@@ -436,22 +585,26 @@ def main():
             rf["traffic_over_algorithmic"] = round((rd + wr) / alg_bytes, 4)
             cyc = pc["GRBM_GUI_ACTIVE"] / 8.0                       # kernel cycles
             simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+            site_n = pc["_sites_per_launch"]
             rf["valu"] = {
-                "insts_per_site": round(pc["SQ_INSTS_VALU"] / S, 1),
-                "salu_per_site": round(pc["SQ_INSTS_SALU"] / S, 1),
-                "lds_per_site": round(pc["SQ_INSTS_LDS"] / S, 1),
-                # VALU issue fraction: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
-                "issue_frac": round(2.0 * pc["SQ_INSTS_VALU"] / (cyc * simds), 4) if cyc else None,
+                "insts_per_site": round(pc["SQ_INSTS_VALU"] / site_n, 1),
+                "salu_per_site": round(pc["SQ_INSTS_SALU"] / site_n, 1),
+                "lds_per_site": round(pc["SQ_INSTS_LDS"] / site_n, 1),
+                "issue_frac_lower_bound": round(2.0 * pc["SQ_INSTS_VALU"] / (cyc * simds), 4) if cyc else None,
+                "issue_frac_assumes": "2 SIMD cycles per wave64 VALU instruction (the multi-wave rate of v_fma_f32 "
+                                      "in MI355X_MICROARCH.md); f64, DPP and transcendental instructions take "
+                                      "longer, so the true VALU busy share is higher",
                 "wave_cycles_split": {k: round(pc[c] / pc["SQ_WAVE_CYCLES"], 3) for k, c in
                                       (("issue", "SQ_ACTIVE_INST_ANY"), ("issue_stall", "SQ_WAIT_INST_ANY"),
                                        ("waitcnt", "SQ_WAIT_ANY"))} if pc["SQ_WAVE_CYCLES"] else None,
                 "clock_ghz_est": round(cyc / (avg_kernel_ms * 1e-3) / 1e9, 3) if avg_kernel_ms else None,
-                "source": "rocprofv3 --pmc, separate passes, same batch, mean of launches 2..",
+                "source": "rocprofv3 --pmc, separate passes over a child scoring the same launches: "
+                          "per-launch means of the second pass",
             }
     if rank == 0 and world == 1 and not args.no_cpu:
-        pre = score[0][: args.cpu_sample].cpu().numpy() if S >= args.cpu_sample else None
-        result["cpu_baseline"] = cpu_baseline(args.lt, args.ln, min(args.cpu_sample, S), args.seed, pre)
-        allc = cpu_baseline_all_cores(args.lt, args.ln, args.seed)
+        result["cpu_baseline"] = cpu_baseline(args.lt, args.ln, sample, args.seed, pre)
+        allc = cpu_baseline_all_cores(args.lt, args.ln, args.seed,
+                                      per_proc=depth_scaled(500_000, args.lt, args.ln))
         if allc:
             result["cpu_baseline_all_cores"] = allc
     if rank == 0:

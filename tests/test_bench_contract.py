@@ -7,35 +7,65 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GRCH38_NAMES = [("chr%s" % c, 0) for c in list(range(1, 23)) + ["X", "Y"]]
+GRCH38 = [248956422, 242193529, 198295559, 190214555, 181538259, 170805979, 159345973, 145138636, 138394717,
+          133797422, 135086622, 133275309, 114364328, 107043718, 101991189, 90338345, 83257441, 80373285,
+          58617616, 64444167, 46709983, 50818468, 156040895, 57227415]
 
 
 @pytest.mark.gpu
 def test_bench_json_contract():
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--sites", "262144", "--steps", "2",
-                        "--warmup", "1", "--cpu-sample", "20000"], capture_output=True, text=True, timeout=600)
+    """Default workload (C4, contig-sharded GRCh38, here / 4096): the driver's
+    fields, strong scaling, the roofline of the timed launches, the weak line
+    and the 1-core reference baseline with its parity spot check."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--c4-scale", "4096", "--steps", "2",
+                        "--warmup", "1", "--cpu-sample", "20000", "--weak-sites", "262144", "--weak-steps", "2"],
+                       capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
-              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "weak_scaling"):
         assert k in r, k
     assert r["n_gpus"] == 1 and r["steps"] == 2 and r["value"] > 1e8 and r["higher_is_better"] is True
-    assert r["scaling"] == "weak" and r["unit"] == "sites/s" and "workload" in r["config"]
+    assert r["scaling"] == "strong" and r["unit"] == "sites/s" and r["config"]["workload"].startswith("C4")
+    genome = r["config"]["genome_sites_per_step"]
+    assert genome == sum(-(-length // 4096) for length in GRCH38)
+    assert r["ranks"][0]["sites"] == 2 * genome and len(r["ranks"][0]["contigs"]) == 24
+    assert abs(r["value"] - 2 * genome / (r["ms_per_step"] * 2e-3)) / r["value"] < 1e-3
     rf = r["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
-    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 and rf["launches_timed"] == 2 * 24
     import shutil
     if shutil.which("rocprofv3") or os.path.exists("/opt/rocm/bin/rocprofv3"):
         # live PMC passes: HBM traffic of the timed kernel and its VALU issue share
         assert rf["traffic"] and 0.5 < rf["traffic_over_algorithmic"] < 3.0, rf
         v = rf["valu"]
-        assert v["insts_per_site"] > 50 and 0 < v["issue_frac"] < 1.0, v
+        assert v["insts_per_site"] > 50 and 0 < v["issue_frac_lower_bound"] < 1.0, v
     cb = r["cpu_baseline"]
     assert cb["cores"] == 1 and cb["value"] > 0 and cb["parity_vs_gpu"] is True
+    assert r["weak_scaling"]["scaling"] == "weak" and r["weak_scaling"]["value"] > 1e8
+
+
+@pytest.mark.gpu
+def test_bench_shard_workload_depth_baseline():
+    """--workload shard (the C2/C3/C5 depth runs): weak scaling, and the CPU
+    baseline is taken at the run's own depth with its parity spot check."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "shard", "--lt", "500",
+                        "--ln", "500", "--sites", "65536", "--steps", "2", "--warmup", "1", "--no-pmc",
+                        "--cpu-sample", "3000"], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["scaling"] == "weak" and r["config"]["sites_per_step_per_gpu"] == 65536
+    assert r["roofline"]["kernel"] == "ss_score_wide"
+    cb = r["cpu_baseline"]
+    assert "500.0xT/500.0xN" in cb["sample"] and cb["parity_vs_gpu"] is True
 
 
 # ---------------------------------------------------------------- CPU: launcher
 def _bench():
     sys.path.insert(0, ROOT)
+    from __graft_entry__ import load_package
+    load_package()                     # registers somatic_sniper_amd (sharding) for bench.c4_layout
     import bench
     return bench
 
@@ -83,18 +113,42 @@ def test_tuning_variables_refused():
 
 
 @pytest.mark.gpu
-def test_bench_gpus2_self_spawned_gloo():
-    """--gpus 2 launched directly: two ranks (sharing the box's one GPU under
-    gloo), each scoring its own shard; whole-job sites over the max rank time."""
+@pytest.mark.parametrize("gpus", [2, 8])
+def test_bench_c4_ranks_self_spawned_gloo(gpus):
+    """--gpus N launched directly, C4 workload: N ranks (sharing the box's one
+    GPU under gloo), each scoring the contigs sharding.shard_contigs gives it;
+    every contig is scored exactly once, and the whole genome's sites over the
+    max rank time is the value."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
-                        "--sites", "262144", "--steps", "2", "--warmup", "1"], env=env,
-                       capture_output=True, text=True, timeout=600)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo",
+                        "--c4-scale", "8192", "--steps", "2", "--warmup", "1", "--weak-sites", "65536",
+                        "--weak-steps", "2"], env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
-    assert r["n_gpus"] == 2 and len(r["ranks"]) == 2
-    assert sorted(x["rank"] for x in r["ranks"]) == [0, 1]
-    assert r["value"] > 0 and "cpu_baseline" not in r
+    assert r["n_gpus"] == gpus and len(r["ranks"]) == gpus and r["scaling"] == "strong"
+    assert sorted(x["rank"] for x in r["ranks"]) == list(range(gpus))
+    contigs = [c for x in r["ranks"] for c in x["contigs"]]
+    assert sorted(contigs) == sorted(n for n, _ in GRCH38_NAMES) and len(set(contigs)) == 24
+    genome = r["config"]["genome_sites_per_step"]
+    assert sum(x["sites_per_step"] for x in r["ranks"]) == genome
+    assert r["value"] > 0 and "cpu_baseline" not in r and r["weak_scaling"]["value"] > 0
     worst = max(x["ms_per_step"] for x in r["ranks"])
     assert abs(r["ms_per_step"] - worst) < 1e-3 + 1e-6 * worst
-    assert abs(r["value"] - 2 * 262144 * 2 / (worst * 2 * 1e-3)) / r["value"] < 1e-3
+    assert abs(r["value"] - genome * 2 / (worst * 2 * 1e-3)) / r["value"] < 1e-3
+    assert r["config"]["plan_imbalance"] < (1.01 if gpus == 8 else 1.001)
+
+
+def test_c4_layout_partitions_the_genome():
+    """CPU: the C4 plan covers every GRCh38 contig exactly once at 1..8 ranks,
+    sized by --c4-scale, and balances the 8-GPU split to within 1% (greedy LPT
+    alone leaves the largest rank 3.6% over the mean)."""
+    b = _bench()
+    for world in (1, 2, 3, 4, 8):
+        names, sizes, plan = b.c4_layout(16, world)
+        assert sorted(t for p in plan for t in p) == list(range(24))
+        assert sizes == [-(-length // 16) for length in GRCH38]
+        loads = [sum(sizes[t] for t in p) for p in plan]
+        assert max(loads) / (sum(loads) / world) < (1.01 if world == 8 else 1.001)
+    import importlib
+    sh = importlib.import_module("somatic_sniper_amd.sharding")
+    assert sh.plan_imbalance(GRCH38, sh.shard_contigs(GRCH38, 8, restarts=0)) < 1.04

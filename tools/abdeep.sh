@@ -10,7 +10,7 @@ for V in "$@"; do
   for cfg in "1200 1000 65536" "3000 3000 16384"; do
     set -- $cfg
     out=$R/gpurun_out/ab/deep_${V}_$1.log
-    SNIPER_AMD_LIB=$L timeout -k 10 200 python "$R/bench.py" --no-cpu --no-pmc --steps 10 --warmup 2 \
+    SNIPER_AMD_LIB=$L timeout -k 10 200 python "$R/bench.py" --workload shard --no-cpu --no-pmc --steps 10 --warmup 2 \
         --lt "$1" --ln "$2" --sites "$3" > "$out" 2>&1 || { echo "$V $1 timing failed"; exit 1; }
     echo "$V ${1}x/${2}x $3 sites: $(python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('%.3e sites/s, deep %.3f ms' % (r['value'], r['roofline']['avg_ms_by_kernel']['deep']))" "$out")"
   done

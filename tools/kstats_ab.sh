@@ -9,7 +9,7 @@ for V in "$@"; do
   mkdir -p "$O"
   SNIPER_AMD_LIB=$R/somatic-sniper_amd/build/libsniper_amd_$V.so timeout -k 10 300 \
     rocprofv3 --kernel-trace --stats --output-format csv -d "$O" -o run -- \
-    python3 "$R/bench.py" --no-cpu --no-pmc --steps 5 --warmup 2 --lt ${LT:-500} --ln ${LN:-500} --sites ${SITES:-262144} \
+    python3 "$R/bench.py" --workload shard --no-cpu --no-pmc --steps 5 --warmup 2 --lt ${LT:-500} --ln ${LN:-500} --sites ${SITES:-262144} \
     > "$O/bench.log" 2>&1 || { echo "$V failed"; exit 1; }
   S=$(find "$O" -name '*kernel_stats.csv' | head -1)
   echo "== $V $(grep '^{"metric"' $O/bench.log | python3 -c 'import json,sys; print("%.3e sites/s" % json.loads(sys.stdin.read())["value"])')"

@@ -14,6 +14,6 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_IN
            "SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$O/pass$i" -o run -- \
-      python3 "$R/bench.py" --pmc-child --sites "$SITES" --lt "$LT" --ln "$LN" > "$O/pass$i.log" 2>&1
+      python3 "$R/bench.py" --pmc-child --workload shard --sites "$SITES" --lt "$LT" --ln "$LN" > "$O/pass$i.log" 2>&1
   python3 "$R/tools/pmc_kernels.py" "$O/pass$i" --sites "$SITES"
 done
