@@ -40,7 +40,7 @@ struct ss_ctx {
     /* model on the device */
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
-    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count */
+    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6] deep total */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
     uint32_t *d_deep_seg;     /* per-main-wave deep segment lengths */
@@ -251,26 +251,24 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         return SS_E_INVAL;
     if (o->calls && !o->n_calls) return SS_E_INVAL;
     HIPCHK(hipSetDevice(c->device));
-    /* main kernel: 4 waves per workgroup, one 16-site block per wave per
-     * iteration, grid-strided; 4 workgroups fit a CU (LDS).  128 per CU gives
-     * each CU 32 rounds of short-lived waves: the dispatcher's refill balances
-     * the load and keeps co-resident waves in different phases (sort / fold /
-     * gathers) -- measured +5.5% over 4 rounds.  Each wave owns a deep-list
-     * segment as long as the most blocks it can visit, times 16 sites. */
-    const uint64_t site_blocks = (b->n_sites + 15) / 16;
+    /* main kernel: 4 waves per workgroup, one 64-site block per wave per
+     * iteration (lane = site), grid-strided; 4 workgroups fit a CU (LDS).
+     * Each wave owns a deep-list segment as long as the most blocks it can
+     * visit, times 64 sites. */
+    const uint64_t site_blocks = (b->n_sites + SS_MAIN_SITES - 1) / SS_MAIN_SITES;
     const uint64_t wpb = SS_MAIN_BLOCK / 64;              /* waves per workgroup */
     uint64_t blocks = (site_blocks + wpb - 1) / wpb;
     const uint64_t max_blocks = (uint64_t)c->n_cu * SS_MAIN_GRID_PER_CU;
     if (blocks > max_blocks) blocks = max_blocks;
     const uint64_t nseg = blocks * (SS_MAIN_BLOCK / 64);
-    const uint64_t seg_cap = (site_blocks + nseg - 1) / nseg * 16;
+    const uint64_t seg_cap = (site_blocks + nseg - 1) / nseg * SS_MAIN_SITES;
     hipStream_t s = (hipStream_t)stream;
     /* one launch at a time per context (shared work lists and counters) */
     if (c->launched && s != c->last_stream) HIPCHK(hipStreamWaitEvent(s, c->done, 0));
     int rc = ensure_deep_cap(c, nseg * seg_cap, s);
     if (rc) return rc;
-    /* counters: deep2 (err is sticky until ss_ctx_check) */
-    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, sizeof(uint32_t), s));
+    /* counters: deep2, deep total (err is sticky until ss_ctx_check) */
+    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 2 * sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
     memset(&a, 0, sizeof(a));
@@ -293,6 +291,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.deep_cap = c->deep_cap;
     a.deep2_list = c->d_deep_list + c->deep_cap;
     a.deep2_count = c->d_counters + 5;
+    a.deep_total = c->d_counters + 6;
     a.err = c->d_counters + 2;
     a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;

@@ -62,9 +62,10 @@ struct ss_score_args {
     ss_glf_t  *glf;
     uint32_t  *n_clamped;
     /* work lists (device; counters zeroed per launch) */
-    uint32_t  *deep_list;     /* sites deeper than the main-kernel limit: one segment of
-                                 deep_seg_cap entries per main-kernel wave, no atomics */
+    uint32_t  *deep_list;     /* sites the main kernel's per-lane path does not score: one
+                                 segment of deep_seg_cap entries per main-kernel wave, no atomics */
     uint32_t  *deep_seg_n;    /* [deep_nseg] entries each main wave wrote (every wave writes) */
+    uint32_t  *deep_total;    /* sum of deep_seg_n (zeroed per launch): 0 lets the wide kernel exit at once */
     uint32_t   deep_seg_cap;
     uint32_t   deep_nseg;     /* = main-kernel waves */
     uint32_t   deep_cap;      /* deep2 list capacity (>= n_sites: cannot overflow) */
@@ -78,7 +79,8 @@ struct ss_score_args {
 #define SS_KERR_MALFORMED      8u   /* decreasing or out-of-range read offsets: the site scored -2 */
 
 /* Launch geometry constants shared with the host. */
-#define SS_MAIN_BLOCK      256   /* 4 waves                                    */
+#define SS_MAIN_BLOCK      256   /* 4 waves, each 64 sites at a time (lane = site) */
+#define SS_MAIN_SITES      64    /* sites per main-kernel wave block           */
 #define SS_MAIN_GRID_PER_CU 128  /* main-kernel workgroups per CU: 4 resident, 32 rounds of short-lived waves (+5.5% over 16) */
 #define SS_DEEP_BLOCK      256
 #define SS_WIDE_BLOCK      512   /* 8 waves, one workgroup per CU (LDS)          */

@@ -34,37 +34,10 @@
 /* Fixed tuning of the shipped kernels (each measured on MI355X):
  * one code path per choice, no run-time or build-time alternatives. */
 #define SS_FOLD_UNROLL 8  /* fold loop unroll (2 -> 8: +0.5% main, +4% at 500x/500x) */
-#define SS_PRIO_SORT 3    /* wave priority raised over the sort network (+1.8%) */
 #define SS_PRIO_WIDE 1    /* the same over the wide kernel's network (+3.7% at 500x/500x) */
 /* `#pragma unroll N` with N from a macro: the count reaches the pragma expanded */
 #define SS_PRAGMA(x) _Pragma(#x)
 #define SS_UNROLL(n) SS_PRAGMA(unroll n)
-#ifndef SS_STAMP
-#define SS_STAMP 0        /* profiling builds only (make variant): per-phase s_memtime cycle totals */
-#endif
-
-/* Phase stamps (SS_STAMP builds only): wave-uniform cycle accumulators,
- * summed over waves into ss_stamp_acc at exit; read by ss_debug_stamps(). */
-#define SS_NSTAMP 16
-#if SS_STAMP
-__device__ unsigned long long ss_stamp_acc[SS_NSTAMP];
-struct Stamps {
-    uint64_t prev, acc[SS_NSTAMP];
-    __device__ void start() { prev = __builtin_amdgcn_s_memtime(); for (int i = 0; i < SS_NSTAMP; ++i) acc[i] = 0; }
-    __device__ void mark(int i) { const uint64_t t = __builtin_amdgcn_s_memtime(); acc[i] += t - prev; prev = t; }
-    __device__ void flush() {
-        if (__lane_id() == 0)
-            for (int i = 0; i < SS_NSTAMP; ++i) atomicAdd(&ss_stamp_acc[i], (unsigned long long)acc[i]);
-    }
-};
-#else
-struct Stamps {
-    __device__ void start() {}
-    __device__ void mark(int) {}
-    __device__ void flush() {}
-};
-#endif
-
 namespace {
 
 /* --------------------------------------------------------------------------
@@ -89,17 +62,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); /* row_bcast:15 */
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); /* row_bcast:31 */
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-/* sums over lanes 0..31 and 32..63 (returned in lanes 31 and 63) */
-__device__ __forceinline__ uint32_t wave_halfsums(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); /* row_shr:1 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); /* row_shr:2 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); /* row_shr:4 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); /* row_shr:8 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); /* row_bcast:15 */
-    return v;
 }
 
 struct SlotRes {
@@ -473,36 +435,19 @@ __device__ __forceinline__ void store_glf(ss_glf_t *dst, uint32_t ref16, const u
 }
 
 /* --------------------------------------------------------------------------
- * Main kernel.
+ * Wave-parallel site machinery of the wide kernel (sites past the main
+ * kernel's per-lane network): 16-bit order keys, the packed
+ * wave-wide bitonic network, 8-bit fold records, the two-lane ordered fold
+ * and the sub-group finish (likelihoods, quantisation, decision).
  *
- * A wave walks 16-site BLOCKS (grid-strided).  A block's reads are contiguous
- * in both CSR arrays, so a run of its sites ("sub-group") is staged into LDS
- * with LDS-DMA (global_load_lds, no VGPRs) as [tumor reads | normal reads];
- * the DMA of the next sub-group is issued after this one's fold and lands
- * while the likelihood/decision phases run.
- *
- * Phase A, per site: ONE wave-wide bitonic sort of 16-bit keys packed two per
- * VGPR covers both samples (sample bit on top):
- *   sample<<15 | base<<13 | minq<<5 | hasbase<<4 | strand<<3 | t
- * where t in 0..6 encodes baseQ relative to 64/128/192 when minq < 4 (the only
- * case where the reference's baseQ tie-break changes the clamped q, see
- * read_key16) and 0 otherwise.  Inside one (sample, base) group the reference's
- * descending key walk visits elements in exactly this order up to swaps of
- * elements with identical (q, strand), which leave every float sum unchanged.
- * Sorted keys are turned into 16-bit fold records (q | strand<<8) and written
- * back over the site's own staged reads (tumor records into its tumor run,
- * normal records into its normal run).
- *
- * Phases B+C: lane (site, sample) walks its sample's four base groups (longest
- * first, so the wave-wide trip count is set by one long chain per lane) and
- * then evaluates the 10 genotypes.  Phase D: lane s decides site s.
+ * 16-bit order key of a read (read_key16):
+ *   sample<<15 | base<<13 | minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz
+ * Inside one (sample, base) group the reference's descending key walk
+ * (sniper_maqcns.c:157-172) visits elements in exactly this order up to swaps
+ * of elements with identical (q, strand), which leave every float sum
+ * unchanged.
  * ------------------------------------------------------------------------ */
-#define GB 16               /* sites per block                 */
-#define STG 2048            /* staged u32 per wave             */
-#define PK_MAX 512          /* nT + nN handled by the packed sort (K <= 4) */
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) const void glb_void_t;
+#define GB 16               /* sites per wide-kernel sub-group */
 
 struct Slot3 {
     uint32_t rec_n;      /* u32 index of the fold records | non-deleted depth << 16 */
@@ -511,14 +456,6 @@ struct Slot3 {
     uint32_t rms;        /* sum of min(mapQ & 0x7f, cap)^2 */
 };
 
-
-struct MainLds {
-    uint32_t stage[SS_MAIN_BLOCK / 64][STG];
-    Slot3    slot[SS_MAIN_BLOCK / 64][2 * GB];
-    SlotRes  res[SS_MAIN_BLOCK / 64][2 * GB];
-    uint32_t site[SS_MAIN_BLOCK / 64][GB];
-    uint32_t refc[SS_MAIN_BLOCK / 64][GB];
-};
 
 /* 16-bit order key (see the section comment); 0xffff = no contribution or pad.
  *   sample<<15 | base<<13 | minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz
@@ -544,8 +481,10 @@ __device__ __forceinline__ uint32_t read_key16(uint32_t rd, uint32_t tb, uint32_
     const uint32_t key = samplebit | base << 13 | minq << 5 | hb << 4 | st << 3 | E << 1 | nz;
     /* a contributing normal read can have every field at its maximum (mapQ =
      * baseQ = 255, T, reverse): 0xfffe keeps it below the pad key, and for
-     * minq >= 4 the E / nz bits only order reads of equal (q, strand) */
-    return (minq | lo6) != 0u ? min(key, 0xfffeu) : 0xffffu;
+     * minq >= 4 the E / nz bits only order reads of equal (q, strand).  A read
+     * with clamped q = 0 gets 0xffff: an OR with the mask rather than a select,
+     * which the compiler turned into a branch around the key arithmetic. */
+    return min(key, 0xfffeu) | ((minq | lo6) != 0u ? 0u : 0xffffu);
 }
 
 /* per-site base tables of read_key16 (bam_nt16_nt4_table semantics,
@@ -557,17 +496,6 @@ __device__ __forceinline__ void nt_tables(uint32_t ref16, uint32_t &tb, uint32_t
     constexpr uint32_t TH = 1u << 2 | 1u << 4 | 1u << 8 | 1u << 16;
     tb = TB | ((TB >> (2u * ref16)) & 3u);
     th = TH | ((TH >> (2u * ref16)) & 1u);
-}
-
-/* fold record of a sorted key (u32):
- *   bits 0..7   clamped q (sniper_maqcns.c:165)   -- esum multiplier
- *   bit  16     1                                  -- fsum multiplier
- *   bits 24..31 strand << 4 (the field offset of its w counter, see fold_sample) */
-__device__ __forceinline__ uint32_t key_to_rec(uint32_t k)
-{
-    /* q = (minq < 4 && nz) ? 4 : minq  ==  max(minq, nz * 4) */
-    const uint32_t q = max((k >> 5) & 0xffu, (k & 1u) << 2);
-    return q | 1u << 16 | (k & 8u) << 25;
 }
 
 /* 8-bit fold record (wide kernel: twice the sites of a 16-bit record in the
@@ -595,10 +523,6 @@ __device__ __forceinline__ bool wide_q_fits(const uint32_t (&v)[1][K])
 }
 
 template <typename RecT> struct RecForm;
-template <> struct RecForm<uint32_t> {
-    static __device__ __forceinline__ uint32_t shift(uint32_t r) { return r >> 24; }
-    static constexpr uint32_t ONE_BIT = 16u, QBITS = 8u;
-};
 template <> struct RecForm<uint8_t> {
     static __device__ __forceinline__ uint32_t shift(uint32_t r) { return (r >> 2) & 16u; }
     static constexpr uint32_t ONE_BIT = 7u, QBITS = 6u;
@@ -693,17 +617,6 @@ __device__ __forceinline__ uint32_t cx_lanes(uint32_t x, uint32_t o)
  * first one's result through dst_unused:UNUSED_PRESERVE; back to back that
  * read is stale on gfx950 (measured), so either one independent instruction
  * (cx_halves2: two registers interleaved) or one wait state separates them. */
-__device__ __forceinline__ uint32_t cx_halves(uint32_t x)
-{
-    uint32_t r;
-    asm volatile("v_max_u16_sdwa %0, %1, %1 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
-                 "s_nop 0\n\t"
-                 "v_min_u16_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1"
-                 : "=&v"(r)
-                 : "v"(x));
-    return r;
-}
-
 __device__ __forceinline__ void cx_halves2(uint32_t &x0, uint32_t &x1)
 {
     uint32_t r0, r1;
@@ -724,7 +637,7 @@ __device__ __forceinline__ void halves_all(uint32_t (&v)[M][K])
     constexpr int N = M * K;
 #pragma unroll
     for (int i = 0; i + 1 < N; i += 2) cx_halves2(v[i / K][i % K], v[(i + 1) / K][(i + 1) % K]);
-    if constexpr (N & 1) v[M - 1][K - 1] = cx_halves(v[M - 1][K - 1]);
+    static_assert((N & 1) == 0, "registers come in pairs");
 }
 
 /* half cleaners e <-> e ^ j for j = J, J/2, ..., 1 (compile-time recursion);
@@ -845,29 +758,6 @@ __device__ __forceinline__ bool split_fits(uint32_t nt, uint32_t nn)
     return nt <= 64u * K && nn <= 64u * K;
 }
 
-/* number of u16 keys (both halves of all K registers) below x, wave-wide.
- * The empty asm pins the count where it is computed: otherwise the scheduler
- * clusters all the compares and keeps every 64-bit ballot live (SGPR spills). */
-template <int K>
-__device__ __forceinline__ uint32_t count_below(const uint32_t (&v)[K], uint32_t x)
-{
-    uint32_t c = 0;
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-        c += (uint32_t)__popcll(__ballot((v[r] & 0xffffu) < x));
-        c += (uint32_t)__popcll(__ballot((v[r] >> 16) < x));
-    }
-    asm volatile("" : "+s"(c));
-    return c;
-}
-
-/* Phase A for M sites at once (independent networks interleaved): each
- * site's staged reads are keyed, sorted, and its fold records are written
- * back over them (u16 view); slot[2m], slot[2m+1] receive its bookkeeping. */
-struct SiteA {
-    uint32_t bt, nt, bn, nn, ref16;
-};
-
 /* Group sizes (sample, base) do not depend on the order, so they are counted
  * from the keys before the sort, next to the rms sums: each contributing key
  * adds one to its base's field of a per-lane counter (8-bit fields when a
@@ -911,144 +801,6 @@ struct GroupCount {
         else return (w[b >> 1] >> (16 * (b & 1))) & 0xffffu;
     }
 };
-
-template <int K, int M>
-__device__ __forceinline__ void sort_sites(uint32_t *stage, const SiteA (&S)[M], uint32_t cap,
-                                           Slot3 *slot, Stamps &st)
-{
-    const uint32_t lane = lane_id();
-    uint32_t v[M][K];
-    uint32_t rs_t[M], rs_n[M];
-    GroupCount<K> gc[M];
-    /* input placement (the two elements of a lane are adjacent reads of ONE
-     * sample and come from LDS with one ds_read2; a pad element is invalid) */
-    bool split = true;
-#pragma unroll
-    for (int m = 0; m < M; ++m) split = split && split_fits<K>(S[m].nt, S[m].nn);
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        const uint32_t nt = S[m].nt, nn = S[m].nn, ntr = nt + (nt & 1u);
-        uint32_t tb, th;
-        nt_tables(S[m].ref16, tb, th);
-        uint32_t a_t = 0, a_n = 0;
-        if constexpr (K == 1) gc[m].zero();
-#pragma unroll
-        for (int r = 0; r < K; ++r) {
-            /* i0: index of the lane's first read within its sample.  Split:
-             * lanes 0..31 (network elements < 64K) take the tumor, 32..63 the
-             * normal.  Otherwise reads are spread over all lanes (the network
-             * is indifferent to its input order). */
-            const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
-            const uint32_t es = ((uint32_t)r * 32u + (lane & 31u)) * 2u;
-            const bool tum = split ? lane < 32u : e0 < ntr;
-            const uint32_t i0 = split ? es : (tum ? e0 : e0 - ntr);
-            const uint32_t idx = i0 + (tum ? S[m].bt : S[m].bn);
-            const uint32_t lim = tum ? nt : nn;
-            const uint32_t rd0 = stage[idx], rd1 = stage[idx + 1u];
-            const uint32_t sb = tum ? 0u : 0x8000u;
-            uint32_t k0 = read_key16(rd0, tb, th, sb);
-            uint32_t k1 = read_key16(rd1, tb, th, sb);
-            const bool in0 = i0 < lim, in1 = i0 + 1u < lim;
-            k0 = in0 ? k0 : 0xffffu;
-            k1 = in1 ? k1 : 0xffffu;
-            const uint32_t t0 = min(rd0 & 0x7fu, cap), t1 = min(rd1 & 0x7fu, cap);
-            const uint32_t x = (in0 ? t0 * t0 : 0u) + (in1 ? t1 * t1 : 0u);
-            a_t += tum ? x : 0u;                      /* tumor part (non-split) */
-            a_n += x;                                 /* both samples */
-            if constexpr (K == 1) gc[m].add(k0, k1, tum);
-            v[m][r] = k0 | k1 << 16;
-        }
-        rs_t[m] = a_t;
-        rs_n[m] = a_n;
-    }
-    st.mark(7);
-    if (SS_PRIO_SORT) __builtin_amdgcn_s_setprio(SS_PRIO_SORT);
-    packed_bitonic_flip<M, K>(v, !split);
-    if (SS_PRIO_SORT) __builtin_amdgcn_s_setprio(0);
-    st.mark(8);
-    uint32_t *rec = stage;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        const uint32_t nt = S[m].nt, nn = S[m].nn, bt = S[m].bt, bn = S[m].bn;
-        /* boundaries c1..c8 of the (sample, base) groups in the sorted
-         * network: at K = 1 from the group sizes counted before the sort (8-bit
-         * fields, one word per sample); at K = 2, 4 by ballot over the sorted
-         * keys (a sample's 256 reads can overflow an 8-bit field, and two-word
-         * counts measured 1.8% slower at 100x/60x) */
-        uint32_t c1, c2, c3, c4, c5, c6, c7, c8;
-        if constexpr (K == 1) {
-            uint32_t wt[1], wn[1];
-            if (split) {                  /* one sample per half-wave */
-                const uint32_t h = wave_halfsums(gc[m].t[0] + gc[m].n[0]);
-                wt[0] = (uint32_t)__builtin_amdgcn_readlane((int)h, 31);
-                wn[0] = (uint32_t)__builtin_amdgcn_readlane((int)h, 63);
-            } else {
-                wt[0] = wave_sum(gc[m].t[0]);
-                wn[0] = wave_sum(gc[m].n[0]);
-            }
-            c1 = GroupCount<K>::field(wt, 0); c2 = c1 + GroupCount<K>::field(wt, 1);
-            c3 = c2 + GroupCount<K>::field(wt, 2); c4 = c3 + GroupCount<K>::field(wt, 3);
-            c5 = c4 + GroupCount<K>::field(wn, 0); c6 = c5 + GroupCount<K>::field(wn, 1);
-            c7 = c6 + GroupCount<K>::field(wn, 2); c8 = c7 + GroupCount<K>::field(wn, 3);
-        } else {
-            c1 = count_below<K>(v[m], 1u << 13); c2 = count_below<K>(v[m], 2u << 13);
-            c3 = count_below<K>(v[m], 3u << 13); c4 = count_below<K>(v[m], 4u << 13);
-            c5 = count_below<K>(v[m], 5u << 13); c6 = count_below<K>(v[m], 6u << 13);
-            c7 = count_below<K>(v[m], 7u << 13); c8 = count_below<K>(v[m], 0xffffu);
-        }
-        st.mark(9);
-        /* fold records back over the staged reads: tumor run, normal run */
-        if (split) {
-            /* one sample per half-wave: a per-lane base, constant offsets */
-            const bool tl = lane < 32u;
-            const uint32_t e0 = lane * (2u * K);
-            const uint32_t lim = tl ? c4 : 64u * K + (c8 - c4);
-            uint32_t *rl0 = rec + ((tl ? bt : bn - 64u * K) + e0);
-#pragma unroll
-            for (int r = 0; r < K; ++r)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (e0 + 2u * r + (uint32_t)h < lim)
-                        rl0[2 * r + h] = key_to_rec((v[m][r] >> (16 * h)) & 0xffffu);
-        } else {
-#pragma unroll
-            for (int r = 0; r < K; ++r) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t e = lane * (2u * K) + 2u * r + (uint32_t)h;
-                    const uint32_t key = (v[m][r] >> (16 * h)) & 0xffffu;
-                    const bool tum = e < c4;
-                    if (e < c8) {
-                        const uint32_t idx = tum ? bt + e : bn + (e - c4);
-                        rec[idx] = key_to_rec(key);
-                    }
-                }
-            }
-        }
-        /* rms sums: split placement has one sample per half-wave */
-        uint32_t rms_t, rms_n;
-        if (split) {
-            const uint32_t h = wave_halfsums(rs_n[m]);
-            rms_t = (uint32_t)__builtin_amdgcn_readlane((int)h, 31);
-            rms_n = (uint32_t)__builtin_amdgcn_readlane((int)h, 63);
-        } else {
-            rms_t = wave_sum(rs_t[m]);
-            rms_n = wave_sum(rs_n[m]) - rms_t;
-        }
-        if (lane == 0) {
-            Slot3 &st_t = slot[2 * m], &st_n = slot[2 * m + 1];
-            st_t.rec_n = bt | nt << 16;
-            st_t.cnt01 = c1 | (c2 - c1) << 16;
-            st_t.cnt23 = (c3 - c2) | (c4 - c3) << 16;
-            st_t.rms = rms_t;
-            st_n.rec_n = bn | nn << 16;
-            st_n.cnt01 = (c5 - c4) | (c6 - c5) << 16;
-            st_n.cnt23 = (c7 - c6) | (c8 - c7) << 16;
-            st_n.rms = rms_n;
-        }
-        st.mark(10);
-    }
-}
 
 /* Fold of one (site, sample) by TWO lanes: role 0 accumulates esum, role 1
  * fsum (sniper_maqcns.c:165-172).  Both run the same instruction stream:
@@ -1122,193 +874,24 @@ __device__ __forceinline__ void fold_sample(const RecT *rec, const uint32_t cnt[
     }
 }
 
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
-/* lanes 0..16: off_t[s..s+16], 17..32: ref[s..s+15], 33..49: off_n[s..s+16],
- * 50, 51: off_t[n_sites], off_n[n_sites] (the batch's read counts), 52: set by
- * begin_block when the block has an offset past the end (every site of the
- * block then goes to the deep lists, whose kernels test each site's own
- * offsets and score a malformed one -2) */
-__device__ __forceinline__ uint32_t load_desc(const ss_score_args &a, uint32_t s)
-{
-    /* The block's bases are wave-uniform (scalar registers); the lane offset is
-     * made opaque here so the compiler cannot hoist per-lane 64-bit pointers
-     * out of the block loop (they would stay live for the whole kernel and
-     * spill to scratch). */
-    uint32_t lane = lane_id();
-    asm volatile("" : "+v"(lane));
-    const uint32_t *ot = a.off_t + s, *on = a.off_n + s;
-    const uint8_t *rf = a.ref + s;
-    const uint32_t rem = (uint32_t)a.n_sites - s;     /* > 0 */
-    uint32_t v = 0;
-    if (lane < 17u) {
-        if (lane <= rem) v = ot[lane];
-    } else if (lane < 33u) {
-        if (lane - 17u < rem) {
-            const uint32_t rc = rf[lane - 17u];
-            v = rc | (uint32_t)ss_tab_nt16(a.m)[rc] << 8;
-        }
-    } else if (lane < 50u) {
-        if (lane - 33u <= rem) v = on[lane - 33u];
-    } else if (lane < 52u) {
-        v = (lane == 50u ? a.off_t : a.off_n)[a.n_sites];
-    }
-    return v;
-}
-#define D_T(i) rl(desc, (i))
-#define D_REF(i) rl(desc, 17u + (i))
-#define D_N(i) rl(desc, 33u + (i))
-
-/* Site sizes of a block (descriptor `desc`), lane i = site i: the inclusive
- * prefix sum of the sites' read counts (DPP row scan over lanes 0..15) and
- * the mask of sites that need more sort slots than the packed main-kernel
- * sort (PK_MAX, incl. the pad element).  Recomputed where needed rather than
- * kept live across the block (register pressure). */
-/* a site the packed main-kernel sort cannot take: too many sort slots.  A
- * decreasing offset (malformed batch) wraps one count to ~2^32, so each
- * sample is also tested on its own: such sites go down the deep lists, whose
- * kernel scores them -2 without a read load. */
-__device__ __forceinline__ bool off_packed(uint32_t t0, uint32_t t1, uint32_t n0, uint32_t n1)
-{
-    const uint32_t nt = t1 - t0, nn = n1 - n0;
-    return nt + (nt & 1u) + nn > PK_MAX || max(nt, nn) > PK_MAX;
-}
-
-struct BlockScan {
-    uint32_t incl;        /* per lane: reads of sites 0..lane */
-    uint64_t deep;        /* wave-uniform */
-};
-
-__device__ __forceinline__ BlockScan scan_block(uint32_t desc, uint32_t nsite)
-{
-    const uint32_t lane = lane_id();
-    /* lane i (< 16): off_t[i] is desc itself, off_t[i + 1] the next lane's
-     * (DPP wave_shl:1); off_n[i] comes from lane 33 + i: lane 32 + i by a
-     * permlane32 swap, then one more wave_shl:1 (no LDS address register) */
-    const auto sw = __builtin_amdgcn_permlane32_swap(desc, desc, false, false);
-    const uint32_t n0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sw[1], 0x130, 0xf, 0xf, false);
-    const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)desc, 0x130, 0xf, 0xf, false);
-    const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n0, 0x130, 0xf, 0xf, false);
-    const uint32_t sz = lane < nsite ? (t1 - desc) + (n1 - n0) : 0u;
-    BlockScan r;
-    const bool alldeep = rl(desc, 52u) != 0u;
-    r.deep = __ballot(lane < nsite && (alldeep || off_packed(desc, t1, n0, n1)));
-    int x = (int)sz;
-    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);    /* row_shr:1 */
-    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);    /* row_shr:2 */
-    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);    /* row_shr:4 */
-    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);    /* row_shr:8 */
-    r.incl = (uint32_t)x;
-    return r;
-}
-
-/* A block becomes current.  An offset past the batch's read count
- * (descriptor lanes 50 / 51 hold off_t[n], off_n[n]) flags the batch
- * malformed and sends the WHOLE block to the deep lists (descriptor lane 52):
- * the wide and deep kernels test each site's own offsets, so a site that
- * runs past the end scores -2 like any other malformed site, and no site of
- * the block is scored on clamped, foreign reads.  The offsets are clamped as
- * well, so no load of this kernel ever leaves the reads.  Then every site too
- * deep for the packed sort is handed to the wide kernel: one list push per
- * block. */
-__device__ __forceinline__ void begin_block(const ss_score_args &a, uint32_t &desc, uint32_t nsite,
-                                            uint32_t sblk, uint32_t *seg, uint32_t &ndeep)
-{
-    const uint32_t lane = lane_id();
-    bool alldeep = false;
-    {
-        const uint32_t end = lane < 17u ? rl(desc, 50u) : rl(desc, 51u);
-        const bool off_lane = lane < 17u || (lane >= 33u && lane < 50u);
-        const bool past = off_lane && desc > end;
-        if (__ballot(past)) {
-            if (lane == 0) atomicOr(a.err, SS_KERR_MALFORMED);
-            desc = past ? end : (lane == 52u ? 1u : desc);
-            alldeep = true;
-        }
-    }
-    const int i = (int)(lane & 15u);
-    const uint32_t t0 = (uint32_t)__shfl((int)desc, i), t1 = (uint32_t)__shfl((int)desc, i + 1);
-    const uint32_t n0 = (uint32_t)__shfl((int)desc, 33 + i), n1 = (uint32_t)__shfl((int)desc, 34 + i);
-    const bool deep = lane < nsite && (alldeep || off_packed(t0, t1, n0, n1));
-    const uint64_t mask = __ballot(deep);
-    if (mask == 0) return;
-    if (deep) {
-        const uint32_t d = ndeep + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-        if (d < a.deep_seg_cap) seg[d] = sblk + lane;
-        else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
-    }
-    ndeep += (uint32_t)__popcll(mask);
-}
-
-struct Sub {
-    uint32_t a, b;        /* site range [a, b) within the block */
-    uint32_t t0, lt;      /* tumor read run  */
-    uint32_t n0, ln;      /* normal read run */
-};
-
-/* staged u32 available to one sub-group: the tumor run is rounded up to a
- * multiple of 4 (16-byte LDS-DMA pieces) before the normal run */
-#define STG_RUNS (STG - 3)
-
-/* Largest run of sites from `pos` whose reads fit one staging buffer; sites
- * too deep for the packed sort (listed by scan_block) are skipped at the
- * start of a run and end it elsewhere.  Wave-parallel over the block. */
-__device__ __forceinline__ Sub form_sub(uint32_t desc, uint32_t nsite, uint32_t pos)
-{
-    const uint32_t lane = lane_id();
-    const BlockScan bs = scan_block(desc, nsite);
-    const uint64_t valid = (1ull << nsite) - 1ull;                 /* nsite <= GB < 64 */
-    const uint64_t nd = ~bs.deep & valid & ~((1ull << pos) - 1ull);
-    Sub r;
-    if (nd == 0) {
-        pos = nsite;
-        r.b = nsite;
-    } else {
-        pos = (uint32_t)__builtin_ctzll(nd);
-        const uint32_t base = pos ? rl(bs.incl, pos - 1u) : 0u;
-        const bool stop = lane > pos && lane < nsite && (((bs.deep >> lane) & 1ull) || bs.incl - base > STG_RUNS);
-        const uint64_t m = __ballot(stop);
-        r.b = m ? (uint32_t)__builtin_ctzll(m) : nsite;
-    }
-    r.a = pos;
-    r.t0 = D_T(pos);
-    r.lt = D_T(r.b) - r.t0;
-    r.n0 = D_N(pos);
-    r.ln = D_N(r.b) - r.n0;
-    return r;
-}
-
-/* offset of the normal run in the stage */
-__device__ __forceinline__ uint32_t normal_base(const Sub &r) { return (r.lt + 3u) & ~3u; }
-
-/* n u32 from src into LDS dst by LDS-DMA: 16-byte pieces, then up to 3 single words */
-__device__ __forceinline__ void dma_run(const uint32_t *src, uint32_t n, uint32_t *dst)
-{
-    const uint32_t lane = lane_id();
-    const uint32_t n4 = n & ~3u;
-    for (uint32_t i = 0; i < n4; i += 256u)
-        if (i + 4u * lane < n4)
-            __builtin_amdgcn_global_load_lds((glb_void_t *)(src + i + 4u * lane), (lds_void_t *)(dst + i), 16, 0, 0);
-    if (lane < n - n4)
-        __builtin_amdgcn_global_load_lds((glb_void_t *)(src + n4 + lane), (lds_void_t *)(dst + n4), 4, 0, 0);
-}
-
-__device__ __forceinline__ void issue_dma(const ss_score_args &a, const Sub &r, uint32_t *buf)
-{
-    dma_run(a.reads_t + r.t0, r.lt, buf);
-    dma_run(a.reads_n + r.n0, r.ln, buf + normal_base(r));
-}
-
 /* Phases B, C, D for the G sites of a sub-group.  Fold records are RecT
- * entries of `recs` (slot rec_n index); `stage` only receives the next DMA. */
+ * entries of `recs` (slot rec_n index). */
 template <typename RecT>
-__device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const RecT *recs, uint32_t *stage,
+__device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const RecT *recs,
                                            const Slot3 *slot, SlotRes *res, const uint32_t *sites,
-                                           const uint32_t *refcs, const double *fk,
-                                           bool have_next, const Sub &nxt, Stamps &st)
+                                           const uint32_t *refcs, const double *fk)
 {
     const uint32_t lane = lane_id();
     const int sl = (int)(lane >> 1);               /* slot = site * 2 + sample */
@@ -1329,7 +912,6 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
     }
     wave_sync();
-    st.mark(3);
     /* exchange esum / fsum within the lane pair (DPP, all lanes active) */
     float es[4], fs[4];
 #pragma unroll
@@ -1352,17 +934,6 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         p[t] = role ? o : mine[t];
         p[5 + t] = role ? mine[t] : o;
     }
-    /* Every fold record has been read and every likelihood gather has
-     * landed: the next sub-group's reads may now stream into the stage while
-     * the glf records and decisions are formed.  (Issued before the gathers,
-     * the DMA was waited for at the first gather: vmcnt drains in issue
-     * order.) */
-    if (have_next) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue_dma(a, nxt, stage);
-    }
-    st.mark(11);
-    st.mark(12);
     if (act && role == 0u) {
         uint32_t lk[10], min_lk, rms_q, cns;
         glf_finish(p, es, depth, rms, a.m, lk, min_lk, rms_q, cns);
@@ -1380,137 +951,427 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         }
     }
     wave_sync();
-    st.mark(4);
     /* the decision reads both samples' records straight from LDS */
     if ((int)lane < G) decide_site(a, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
     wave_sync();
-    st.mark(5);
 }
 
 }  // namespace
 
-/* compiled for 4 waves per SIMD (the VGPR and the LDS budget both allow 4) */
-__global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
+/* --------------------------------------------------------------------------
+ * Main kernel: one LANE per site.
+ *
+ * A wave scores 64 consecutive sites -- lane l takes site l of its block --
+ * and the blocks are grid-strided.  Everything per site runs inside its lane,
+ * serially, so one VALU instruction advances 64 sites:
+ *   1. key build: the site's packed reads (x4 loads straight into registers)
+ *      become 16-bit order keys (read_key16) in a per-lane bitonic network of
+ *      LN_N elements; the rms sums and the group sizes (contributing reads per
+ *      (sample, base)) are accumulated on the way.
+ *   2. sort: the network, in registers, two keys per register: every
+ *      instruction is the compare-exchange of two element pairs
+ *      (v_pk_min_u16 / v_pk_max_u16), no cross-lane traffic.
+ *   3. records: sorted keys become 8-bit fold records (q | strand << 6) in
+ *      LDS, dword-interleaved by lane, so every per-lane index is conflict-free.
+ *   4. fold (sniper_maqcns.c:160-175): per sample, the chain of its largest
+ *      base group, then the other three (usually empty or tiny), each in the
+ *      reference's descending key order: float accumulators fed double
+ *      increments, w counters per strand.
+ *   5. likelihoods, homozygote fix, quantisation, glf2cns per sample
+ *      (:176-273), then the site decision of glf_somatic (somatic_sniper.c).
+ * When every site of the wave has at most LN_N sort slots (tumor rounded up to
+ * 4, then normal) both samples share one network ("joint"); otherwise the
+ * tumor, then the normal is sorted and folded on its own ("separate").  Sites
+ * with more than LN_N reads in a sample, malformed offsets, or a contributing
+ * read of minq >= 64 (the 8-bit record holds q < 64) are listed for the wide
+ * kernel (which hands the last two kinds on to the deep kernel).
+ * ------------------------------------------------------------------------ */
+namespace {
+
+#define LN_N 128                     /* elements of the per-lane network          */
+#define LN_R (LN_N / 2)              /* its packed registers                      */
+#define LN_C (LN_N / 4)              /* 4-element chunks (one x4 load each)       */
+#define LN_G 4                       /* chunks loaded together                    */
+#define LN_WAVES (SS_MAIN_BLOCK / 64)
+
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+struct LaneLds {
+    union {
+        uint32_t rec[LN_C][64];      /* fold record of element e, lane l: byte e & 3 of rec[e >> 2][l] */
+        SlotRes res[64][2];          /* the two samples' results, for the decision */
+    };
+    uint32_t tres[5][64];            /* the tumor's results while the normal is sorted (registers) */
+};
+
+/* Network layout: register r holds element r in its low half and element
+ * N - 1 - r, bit-complemented, in its high half.  A compare-exchange of
+ * elements e < e' puts the minimum at e; for a pair of registers (r, r ^ m)
+ * with r < r ^ m that is a min into r and a max into r ^ m in BOTH halves
+ * (the complement turns the high halves' reversed order into the same
+ * direction), so one v_pk_min_u16 + v_pk_max_u16 pair serves two element
+ * pairs.  The only other stage, element r against N - 1 - r, stays inside
+ * register r: min(lo, ~hi) to lo and its complement ~max to hi. */
+__device__ __forceinline__ void ln_ce(uint32_t &lo, uint32_t &hi)
+{
+    const uint32_t mn = pk_min(lo, hi), mx = pk_max(lo, hi);
+    lo = mn;
+    hi = mx;
+}
+
+__device__ __forceinline__ uint32_t ln_ce_self(uint32_t x)
+{
+    return pk_min_swo(x, ~x);        /* (min(a, b), min(~b, ~a)) for x = (a, ~b) */
+}
+
+template <int R, int M>
+__device__ __forceinline__ void ln_stage(uint32_t (&v)[R])
+{
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if ((r ^ M) > r) ln_ce(v[r], v[r ^ M]);
+}
+
+template <int R, int J>
+__device__ __forceinline__ void ln_clean(uint32_t (&v)[R])
+{
+    if constexpr (J >= 1) {
+        ln_stage<R, J>(v);
+        ln_clean<R, J / 2>(v);
+    }
+}
+
+/* level K of the flip-form bitonic sort: mirror e <-> e ^ (K - 1), then the
+ * half cleaners e <-> e ^ j, j = K/4 .. 1 (every comparator min-to-lower) */
+template <int R, int K>
+__device__ __forceinline__ void ln_levels(uint32_t (&v)[R])
+{
+    if constexpr (K <= 2 * R) {
+        if constexpr (K == 2 * R) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = ln_ce_self(v[r]);
+        } else {
+            ln_stage<R, K - 1>(v);
+        }
+        ln_clean<R, K / 4>(v);
+        ln_levels<R, 2 * K>(v);
+    }
+}
+
+/* sorted element e (ascending) */
+template <int R>
+__device__ __forceinline__ uint32_t ln_elem(const uint32_t (&v)[R], int e)
+{
+    return e < R ? (v[e] & 0xffffu) : (~v[2 * R - 1 - e] >> 16);
+}
+
+/* 8-bit fold record of a key: clamped q (sniper_maqcns.c:165) | strand << 6 */
+__device__ __forceinline__ uint32_t ln_rec(uint32_t k)
+{
+    const uint32_t q = max((k >> 5) & 0xffu, (k & 1u) << 2);
+    return q | (k & 8u) << 3;
+}
+
+/* one pass of the key build: the lane's elements [0, na) are reads pa[0..na),
+ * [na4, na4 + nb) reads pb[0..nb) (na4 = na rounded up to 4, so a chunk of 4
+ * elements comes from one sample), every other element is a pad (0xffff).
+ * sa / sb: the samples' key bits (0 tumor, 0x8000 normal).  Returns the
+ * per-sample rms sums and group sizes (four 8-bit fields, base b at 8b) and
+ * whether a contributing read has minq >= 64.  Every x4 load stays inside
+ * the batch's reads (the caller routes a block that would pass their end to
+ * the wide kernel). */
+struct LaneIn {
+    const uint32_t *ba, *bb;         /* wave-uniform array bases of A and B */
+    uint32_t oa, ob;                 /* the lane's first read in A and in B */
+    uint32_t na, nb, na4, sa, sb;
+    uint32_t tb, th;                 /* read_key16 base tables of the site's ref */
+};
+
+struct LaneAcc {
+    uint32_t rms_a, rms_b, cnt_a, cnt_b;
+    bool wild;
+};
+
+__device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, uint32_t nch, uint32_t cap, uint32_t (&v)[LN_R])
+{
+    LaneAcc acc = {0u, 0u, 0u, 0u, false};
+#pragma unroll
+    for (int r = 0; r < LN_R; ++r) v[r] = 0x0000ffffu;     /* pads: lo 0xffff, hi ~0xffff */
+#pragma unroll
+    for (int g = 0; g < LN_C / LN_G; ++g) {
+        if ((uint32_t)(g * LN_G) >= nch) continue;           /* wave-uniform; no break: the loop
+                                                                must unroll fully (static v indices) */
+        uint32_t x[LN_G][4];
+        int lim[LN_G];
+        bool fa[LN_G];
+#pragma unroll
+        for (int j = 0; j < LN_G; ++j) {
+            const uint32_t c4 = (uint32_t)(4 * (g * LN_G + j));
+            fa[j] = c4 < in.na4;
+            const uint32_t *src = fa[j] ? in.ba + (in.oa + c4) : in.bb + (in.ob + (c4 - in.na4));
+            lim[j] = fa[j] ? (int)in.na - (int)c4 : (int)(in.na4 + in.nb) - (int)c4;
+            u32x4_a4 q4 = {0u, 0u, 0u, 0u};
+            if (lim[j] > 0) q4 = *reinterpret_cast<const u32x4_a4 *>(src);
+            x[j][0] = q4.x; x[j][1] = q4.y; x[j][2] = q4.z; x[j][3] = q4.w;
+        }
+#pragma unroll
+        for (int j = 0; j < LN_G; ++j) {
+            const int c = g * LN_G + j;
+            const uint32_t sb = fa[j] ? in.sa : in.sb;
+            uint32_t crms = 0, ccnt = 0;
+            bool cwild = false;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t rd = x[j][t];
+                const bool valid = t < lim[j];
+                uint32_t key = read_key16(rd, in.tb, in.th, sb);
+                key = valid ? key : 0xffffu;
+                cwild = cwild || (key != 0xffffu && (key & 0x1800u) != 0u);
+                const uint32_t tq = min(rd & 0x7fu, cap);
+                crms += valid ? tq * tq : 0u;
+                ccnt += key != 0xffffu ? 1u << ((key >> 10) & 0x18u) : 0u;
+                const int e = 4 * c + t;
+                if (e < LN_R) v[e] = key;                                     /* hi: a later chunk */
+                else v[LN_N - 1 - e] |= (key ^ 0xffffu) << 16;
+            }
+            acc.rms_a += fa[j] ? crms : 0u;
+            acc.rms_b += fa[j] ? 0u : crms;
+            acc.cnt_a += fa[j] ? ccnt : 0u;
+            acc.cnt_b += fa[j] ? 0u : ccnt;
+            acc.wild = acc.wild || cwild;
+        }
+    }
+    return acc;
+}
+
+/* sorted elements [0, nel) as records into the lane's LDS column */
+__device__ __forceinline__ void ln_records(const uint32_t (&v)[LN_R], uint32_t nel, LaneLds &L, uint32_t lane)
+{
+#pragma unroll
+    for (int i = 0; i < LN_C; ++i) {
+        if ((uint32_t)(4 * i) >= nel) continue;              /* wave-uniform */
+        const uint32_t d = ln_rec(ln_elem(v, 4 * i)) | ln_rec(ln_elem(v, 4 * i + 1)) << 8 |
+                           ln_rec(ln_elem(v, 4 * i + 2)) << 16 | ln_rec(ln_elem(v, 4 * i + 3)) << 24;
+        L.rec[i][lane] = d;
+    }
+}
+
+/* the ordered chain of one (sample, base) group: records [s0, s0 + n),
+ * walked from the top (sniper_maqcns.c:162-172) */
+__device__ __forceinline__ void ln_chain(const LaneLds &L, uint32_t lane, uint32_t s0, uint32_t n,
+                                         const double *fk, float &e, float &f)
+{
+    const uint8_t *col = reinterpret_cast<const uint8_t *>(&L.rec[0][0]) + 4u * lane;
+    e = 0.0f;
+    f = 0.0f;
+    uint32_t W = 0;                  /* strand 0 count in bits 0..15, strand 1 in 16..31 (units of 8 B) */
+    const char *fkb = reinterpret_cast<const char *>(fk);
+    for (uint32_t i = 0; __ballot(i < n); ++i) {
+        if (i < n) {
+            const uint32_t k = s0 + n - 1u - i;
+            const uint32_t r = col[(k >> 2) * 256u + (k & 3u)];
+            const uint32_t sh = (r >> 2) & 16u;                  /* strand << 4 */
+            const uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
+            W += 8u << sh;
+            const double t = *reinterpret_cast<const double *>(fkb + w8);
+            e = (float)((double)e + t * (double)(r & 63u));
+            f = (float)((double)f + t);
+        }
+    }
+}
+
+/* fold of one sample: group sizes cnt (8-bit fields), records from s0 */
+__device__ __forceinline__ void ln_fold(const LaneLds &L, uint32_t lane, uint32_t s0, uint32_t cnt,
+                                        const double *fk, float es[4], float fs[4], uint32_t c[4])
+{
+    uint32_t st[4];
+    uint32_t big = 0, cb = 0, run = s0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        c[b] = (cnt >> (8 * b)) & 0xffu;
+        st[b] = run;
+        run += c[b];
+        if (c[b] > cb) { cb = c[b]; big = (uint32_t)b; }
+    }
+    /* the largest group first (one long chain per lane), then the rest */
+    float e, f;
+    const uint32_t sbig = big == 0 ? st[0] : (big == 1 ? st[1] : (big == 2 ? st[2] : st[3]));
+    ln_chain(L, lane, sbig, cb, fk, e, f);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        float eb, fb;
+        const bool isbig = (uint32_t)b == big;
+        ln_chain(L, lane, st[b], isbig ? 0u : c[b], fk, eb, fb);
+        es[b] = isbig ? e : eb;
+        fs[b] = isbig ? f : fb;
+    }
+}
+
+/* likelihoods .. glf2cns of one sample into r (sniper_maqcns.c:176-273) */
+__device__ __forceinline__ void ln_finish(const float es[4], const float fs[4], const uint32_t craw[4],
+                                          uint32_t n, uint32_t rms, const ss_dev_model &m, uint32_t &lk03,
+                                          uint32_t &lk47, uint32_t &lk89, uint32_t &cns, uint32_t &mq)
+{
+    uint32_t c[4];
+    const uint32_t tot = rescale_counts(craw, c);
+    float p[10];
+    geno_p5(0u, es, fs, c, tot, m, p);
+    geno_p5(1u, es, fs, c, tot, m, p + 5);
+    uint32_t lk[10], min_lk, rms_q;
+    glf_finish(p, es, n, rms, m, lk, min_lk, rms_q, cns);
+    lk03 = lk[0] | lk[1] << 8 | lk[2] << 16 | lk[3] << 24;
+    lk47 = lk[4] | lk[5] << 8 | lk[6] << 16 | lk[7] << 24;
+    lk89 = lk[8] | lk[9] << 8;
+    mq = min_lk | rms_q << 8;
+}
+
+__device__ __forceinline__ void ln_store_res(SlotRes &r, uint32_t lk03, uint32_t lk47, uint32_t lk89, uint32_t cns,
+                                             uint32_t n, uint32_t mq)
+{
+    uint32_t *w = reinterpret_cast<uint32_t *>(r.lk);
+    w[0] = lk03;
+    w[1] = lk47;
+    w[2] = lk89;
+    r.cns = cns;
+    r.depth = n;
+    r.min_lk = (uint8_t)(mq & 0xffu);
+    r.rms_q = (uint8_t)(mq >> 8);
+}
+
+__device__ __forceinline__ void ln_store_glf(ss_glf_t *dst, uint32_t ref16, uint32_t lk03, uint32_t lk47, uint32_t lk89,
+                                             uint32_t mq, uint32_t depth)
+{
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+    d[0] = (ref16 & 0xffu) | (mq >> 8 & 0xffu) << 8 | (lk03 & 0xffffu) << 16;
+    d[1] = lk03 >> 16 | (lk47 & 0xffffu) << 16;
+    d[2] = lk47 >> 16 | lk89 << 16;
+    d[3] = mq & 0xffu;
+    d[4] = depth;
+}
+
+}  // namespace
+
+/* compiled for 3 waves per SIMD: the per-lane network's 64 registers, the
+ * chunk loads in flight and the key arithmetic need about 160 VGPRs (at 128
+ * the compiler spills); the records take 8 KB of LDS per wave */
+__global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(3)))
 void ss_score_main(ss_score_args a)
 {
     __shared__ double fk[256];
-    __shared__ MainLds L;
-    const uint32_t lane = lane_id();
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   /* wave-uniform */
+    __shared__ LaneLds LL[LN_WAVES];
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
-    Stamps st;
-    st.start();
-
-    uint32_t *stage = L.stage[wv];
-    Slot3 *slot = L.slot[wv];
-    SlotRes *res = L.res[wv];
-    uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
-    /* block bookkeeping in 32-bit scalars (n_sites < 2^32, checked on the host) */
-    const uint32_t nwaves = gridDim.x * (SS_MAIN_BLOCK / 64);
+    const uint32_t lane = lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    LaneLds &L = LL[wv];
+    const uint32_t nwaves = gridDim.x * LN_WAVES;
     const uint32_t n_sites = (uint32_t)a.n_sites;
-    const uint32_t nblocks = (n_sites + GB - 1) / GB;
+    const uint32_t nblocks = (n_sites + 63u) / 64u;
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
-
-    uint32_t blk = blockIdx.x * (SS_MAIN_BLOCK / 64) + wv;
-    /* this wave's segment of the deep list; its length is stored on every exit */
-    const uint32_t gw = blk;
+    const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
+    const uint32_t gw = blockIdx.x * LN_WAVES + wv;
     uint32_t *seg = a.deep_list + (size_t)gw * a.deep_seg_cap;
     uint32_t ndeep = 0;
-    if (blk >= nblocks) {
-        if (lane == 0) a.deep_seg_n[gw] = 0u;
-        st.flush();
-        return;
-    }
-    uint32_t desc = load_desc(a, blk * GB);
-    uint32_t nsite = min(n_sites - blk * GB, (uint32_t)GB);
-    uint32_t nblk = blk + nwaves;
-    uint32_t ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-    begin_block(a, desc, nsite, blk * GB, seg, ndeep);
-    Sub cur = form_sub(desc, nsite, 0);
-    while (cur.a == cur.b) {               /* whole block deep */
-        blk = nblk;
-        if (blk >= nblocks) {
-            if (lane == 0) a.deep_seg_n[gw] = ndeep;
-            st.flush();
-            return;
+    for (uint32_t blk = gw; blk < nblocks; blk += nwaves) {
+        const uint32_t s = blk * 64u + lane;
+        const bool insite = s < n_sites;
+        uint32_t ot = 0, ot1 = 0, on = 0, on1 = 0, refc = 'N';
+        if (insite) {
+            ot = a.off_t[s];
+            ot1 = a.off_t[s + 1];
+            on = a.off_n[s];
+            on1 = a.off_n[s + 1];
+            refc = a.ref[s];
         }
-        desc = ndesc;
-        nsite = min(n_sites - blk * GB, (uint32_t)GB);
-        nblk = blk + nwaves;
-        ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-        begin_block(a, desc, nsite, blk * GB, seg, ndeep);
-        cur = form_sub(desc, nsite, 0);
-    }
-    issue_dma(a, cur, stage);
-    st.mark(6);
-
-    for (;;) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the sub-group's reads are in LDS */
-        st.mark(0);
-        /* ---- phase A ---- */
-        int G = 0;
-        for (uint32_t i = cur.a; i < cur.b;) {
-            SiteA S2[2];
-            uint32_t tot[2];
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                const uint32_t j = i + (uint32_t)m < cur.b ? i + (uint32_t)m : i;
-                const uint32_t t_i = D_T(j), n_i = D_N(j);
-                const uint32_t rdesc = D_REF(j);
-                S2[m].nt = D_T(j + 1u) - t_i;
-                S2[m].nn = D_N(j + 1u) - n_i;
-                S2[m].bt = t_i - cur.t0;
-                S2[m].bn = normal_base(cur) + (n_i - cur.n0);
-                S2[m].ref16 = rdesc >> 8;
-                tot[m] = S2[m].nt + (S2[m].nt & 1u) + S2[m].nn;   /* sort slots incl. pad */
-                if (lane == 0 && i + (uint32_t)m < cur.b) {
-                    sites[G + m] = blk * GB + j;
-                    refcs[G + m] = rdesc & 0xffffu;      /* ref char | nt16 << 8 */
+        const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
+        const uint32_t nt = ot1 - ot, nn = on1 - on;
+        const bool formed = ot <= ot1 && ot1 <= end_t && on <= on1 && on1 <= end_n;
+        bool ok = insite && formed && nt <= LN_N && nn <= LN_N;
+        const uint32_t nt4 = (nt + 3u) & ~3u, nn4 = (nn + 3u) & ~3u;
+        /* wave-uniform shape: joint when every ok site fits one network */
+        /* a block whose x4 loads would pass the end of the batch's reads (its
+         * last sites; one block per batch at most) goes to the wide kernel,
+         * which loads read by read */
+        if (__ballot(ok && (ot + nt4 > end_t || on + nn4 > end_n))) ok = false;
+        const bool joint = !__ballot(ok && nt4 + nn > LN_N);
+        uint32_t tb, th;
+        nt_tables(ref16, tb, th);
+        bool wild = false;
+        uint32_t lkN03 = 0, lkN47 = 0, lkN89 = 0, cnsN = 0, mqN = 0;
+        /* joint: one pass, both samples; separate: the tumor, then the normal */
+        for (uint32_t pass = 0; pass < (joint ? 1u : 2u); ++pass) {
+            LaneIn in;
+            in.tb = tb;
+            in.th = th;
+            const bool nrm = pass == 1u;
+            in.ba = nrm ? a.reads_n : a.reads_t;
+            in.oa = nrm ? on : ot;
+            in.na = ok ? (nrm ? nn : nt) : 0u;
+            in.na4 = ok ? (nrm ? nn4 : nt4) : 0u;
+            in.sa = nrm ? 0x8000u : 0u;
+            in.bb = a.reads_n;
+            in.ob = on;
+            in.nb = joint && ok ? nn : 0u;
+            in.sb = 0x8000u;
+            const uint32_t nch = wave_max((in.na4 + in.nb + 3u) >> 2);
+            uint32_t v[LN_R];
+            const LaneAcc acc = ln_keys(in, nch, cap, v);
+            wild = wild || acc.wild;
+            ln_levels<LN_R, 2>(v);
+            ln_records(v, 4u * nch, L, lane);
+            /* fold and finish the pass's samples: A (its records from 0), then
+             * in joint mode B (after A's contributing reads) */
+            const uint32_t ca = acc.cnt_a;
+            const uint32_t tot_a = (ca & 0xffu) + (ca >> 8 & 0xffu) + (ca >> 16 & 0xffu) + (ca >> 24);
+            for (uint32_t k = 0; k < (joint ? 2u : 1u); ++k) {
+                const bool smpN = nrm || k == 1u;
+                float es[4], fs[4];
+                uint32_t c[4];
+                ln_fold(L, lane, k ? tot_a : 0u, k ? acc.cnt_b : acc.cnt_a, fk, es, fs, c);
+                uint32_t l03, l47, l89, cn, mq;
+                ln_finish(es, fs, c, smpN ? nn : nt, k ? acc.rms_b : acc.rms_a, a.m, l03, l47, l89, cn, mq);
+                if (smpN) {
+                    lkN03 = l03; lkN47 = l47; lkN89 = l89; cnsN = cn; mqN = mq;
+                } else {
+                    L.tres[0][lane] = l03; L.tres[1][lane] = l47; L.tres[2][lane] = l89;
+                    L.tres[3][lane] = cn;  L.tres[4][lane] = mq;
                 }
             }
-            if (i + 1u < cur.b && tot[0] <= 256u && tot[1] <= 256u) {   /* two sites, interleaved */
-                if (tot[0] <= 128u && tot[1] <= 128u) sort_sites<1, 2>(stage, S2, cap, slot + 2 * G, st);
-                else sort_sites<2, 2>(stage, S2, cap, slot + 2 * G, st);
-                G += 2;
-                i += 2;
-                continue;
+            wave_sync();                                     /* the pass's records are read */
+        }
+        ok = ok && !wild;
+        /* sites the lane path does not score: the wide kernel's list (one
+         * segment per wave, no atomics) */
+        const uint64_t out = __ballot(insite && !ok);
+        if (out) {
+            if (insite && !ok) {
+                const uint32_t d = ndeep + (uint32_t)__popcll(out & ((1ull << lane) - 1ull));
+                if (d < a.deep_seg_cap) seg[d] = s;
+                else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
             }
-            SiteA S1[1] = {S2[0]};
-            if (tot[0] <= 128u) sort_sites<1, 1>(stage, S1, cap, slot + 2 * G, st);
-            else if (tot[0] <= 256u) sort_sites<2, 1>(stage, S1, cap, slot + 2 * G, st);
-            else sort_sites<4, 1>(stage, S1, cap, slot + 2 * G, st);
-            ++G;
-            ++i;
+            ndeep += (uint32_t)__popcll(out);
+        }
+        if (!formed && insite) atomicOr(a.err, SS_KERR_MALFORMED);
+        const uint32_t dt = nt > 16777215u ? 16777215u : nt, dn = nn > 16777215u ? 16777215u : nn;
+        const uint32_t lkT03 = L.tres[0][lane], lkT47 = L.tres[1][lane], lkT89 = L.tres[2][lane];
+        const uint32_t cnsT = L.tres[3][lane], mqT = L.tres[4][lane];
+        wave_sync();                                         /* res overlays the records */
+        if (ok) {
+            ln_store_res(L.res[lane][0], lkT03, lkT47, lkT89, cnsT, dt, mqT);
+            ln_store_res(L.res[lane][1], lkN03, lkN47, lkN89, cnsN, dn, mqN);
+            if (a.glf) {
+                ln_store_glf(&a.glf[2ull * s], ref16, lkT03, lkT47, lkT89, mqT, dt);
+                ln_store_glf(&a.glf[2ull * s + 1], ref16, lkN03, lkN47, lkN89, mqN, dn);
+            }
         }
         wave_sync();
-        st.mark(1);
-        /* ---- next sub-group: same block, else the next non-empty block ---- */
-        Sub nxt;
-        bool have = false;
-        if (cur.b < nsite) {
-            nxt = form_sub(desc, nsite, cur.b);
-            have = nxt.a < nxt.b;
-        }
-        while (!have) {
-            blk = nblk;
-            if (blk >= nblocks) break;
-            desc = ndesc;
-            nsite = min(n_sites - blk * GB, (uint32_t)GB);
-            nblk = blk + nwaves;
-            ndesc = nblk < nblocks ? load_desc(a, nblk * GB) : 0u;
-            begin_block(a, desc, nsite, blk * GB, seg, ndeep);
-            nxt = form_sub(desc, nsite, 0);
-            have = nxt.a < nxt.b;
-        }
-        st.mark(2);
-        /* ---- phases B + C + D (the next DMA is issued after the fold) ---- */
-        finish_sub<uint32_t>(a, G, stage, stage, slot, res, sites, refcs, fk, have, nxt, st);
-        if (!have) break;
-        cur = nxt;
+        if (ok) decide_site(a, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
+        wave_sync();
     }
-    if (lane == 0) a.deep_seg_n[gw] = ndeep;
-    st.flush();
+    if (lane == 0) {
+        a.deep_seg_n[gw] = ndeep;
+        if (ndeep) atomicAdd(a.deep_total, ndeep);
+    }
 }
 
 /* --------------------------------------------------------------------------
@@ -1736,6 +1597,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
 {
     __shared__ double fk[256];
     __shared__ WideLds L;
+    if (*a.deep_total == 0u) return;          /* the main kernel listed no site (every workgroup) */
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -1745,7 +1607,6 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
     SlotRes *res = L.res[wv];
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
-    const Sub none = {0, 0, 0, 0, 0, 0};
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
     /* the main kernel's per-wave segments, GB entries at a time */
     for (uint32_t sg = blockIdx.x * WIDE_WAVES + wv; sg < a.deep_nseg; sg += gridDim.x * WIDE_WAVES)
@@ -1839,8 +1700,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 ++G;
             }
             wave_sync();
-            Stamps nost;
-            if (G) finish_sub<uint8_t>(a, G, arena, nullptr, slot, res, sites, refcs, fk, false, none, nost);
+            if (G) finish_sub<uint8_t>(a, G, arena, slot, res, sites, refcs, fk);
         }
     }
 }
@@ -1907,12 +1767,6 @@ __device__ __forceinline__ bool site_wellformed(uint32_t o0, uint32_t o1, uint32
     return o0 <= o1 && o1 <= end;
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t v)
-{
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
-}
 
 /* one pass over one sample's reads, eight in flight per lane: counts the
  * reads whose bin falls in [lo, hi) into the window histogram; mode 0 (the
@@ -2191,17 +2045,4 @@ int ss_launch_synth_reads(const ss_synth_k_t &k, uint64_t first, uint64_t n,
     return (int)hipGetLastError();
 }
 
-#if SS_STAMP
-/* diagnostic builds: per-phase cycle totals of ss_score_main (summed over
- * waves), then reset.  Phases: 0 wait for the staged reads, 1 phase A loop
- * remainder, 2 next sub-group, 3 fold, 4 glf finish + stores, 5 decision,
- * 6 prologue, 7 key build, 8 sort network, 9 group counts, 10 record
- * write-back + rms, 11 DMA issue, 12 genotype likelihoods. */
-extern "C" __attribute__((visibility("default"))) int ss_debug_stamps(unsigned long long *out)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ss_stamp_acc), sizeof(unsigned long long) * SS_NSTAMP) != hipSuccess)
-        return -1;
-    static const unsigned long long zero[SS_NSTAMP] = {0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(ss_stamp_acc), zero, sizeof zero) == hipSuccess ? 0 : -1;
-}
-#endif
+
