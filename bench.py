@@ -274,8 +274,8 @@ def sites_per_launch(args) -> float:
     if args.workload == "shard":
         return float(args.sites)
     _, sizes, _ = c4_layout(args.c4_scale, 1)
-    n = [min(args.chunk, s - f) for s in sizes for f in range(0, s, args.chunk)]
-    return float(np.mean(n))
+    total = sum(sizes)                      # make_batches packs the contigs into full launches
+    return total / -(-total // args.chunk)
 
 
 def cpu_model() -> str:
@@ -317,13 +317,26 @@ def make_batches(ctx, pkg, args, rank, world, dev):
     out = []
     if args.workload == "c4":
         names, sizes, plan = c4_layout(args.c4_scale, world)
+        # the rank's contigs back to back (ascending tid), cut into launches of
+        # at most --chunk sites: a launch may hold the end of one contig and the
+        # start of the next (sites are independent; fewer, fuller launches)
+        launches, cur, room = [], [], args.chunk
         for tid in plan[rank]:
-            syn = pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=tid)
-            for first in range(0, sizes[tid], args.chunk):
-                n = min(args.chunk, sizes[tid] - first)
-                d = ctx.synth_device(syn, first, n, device=dev)
-                d.update(tid=tid, first=first)
-                out.append(d)
+            first = 0
+            while first < sizes[tid]:
+                n = min(room, sizes[tid] - first)
+                cur.append((tid, first, n))
+                first += n
+                room -= n
+                if room == 0:
+                    launches.append(cur)
+                    cur, room = [], args.chunk
+        if cur:
+            launches.append(cur)
+        for pieces in launches:
+            d = synth_pieces(ctx, pkg, args, pieces, dev)
+            d.update(tid=pieces[0][0], first=pieces[0][1], pieces=pieces)
+            out.append(d)
     else:
         S = args.sites
         for b in range(args.batches):
@@ -332,6 +345,63 @@ def make_batches(ctx, pkg, args, rank, world, dev):
             d.update(tid=rank, first=b * S)
             out.append(d)
     return out
+
+
+def i32(x: int) -> int:
+    """The int32 with the bits of the u32 x."""
+    return x - (1 << 32) if x >= 1 << 31 else x
+
+
+def synth_pieces(ctx, pkg, args, pieces, dev):
+    """One HBM batch made of synthetic pieces (synth shard = contig, sites
+    [first, first + n)), generated on the device piece by piece straight into
+    the batch's arrays; each piece's read offsets are then moved up by the
+    reads of the pieces before it."""
+    import ctypes as C
+    import torch
+    S = sum(n for _, _, n in pieces)
+    ref = torch.empty(S, dtype=torch.uint8, device=dev)
+    ot = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    on = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    lib = ctx.lib
+    tot = []
+    so = 0
+    torch.cuda.synchronize(dev)
+    for tid, first, n in pieces:                  # pass 1: ref, piece-local offsets, read counts
+        syn = pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=tid)
+        nt, nn = C.c_uint64(), C.c_uint64()
+        rc = lib.ss_synth_batch_device(ctx.h, C.byref(syn), first, n, ref.data_ptr() + so,
+                                       ot.data_ptr() + 4 * so, on.data_ptr() + 4 * so, None, None,
+                                       C.byref(nt), C.byref(nn))
+        if rc:
+            raise pkg.SniperError(rc, "ss_synth_batch_device")
+        tot.append((nt.value, nn.value))
+        so += n
+    T, N = sum(t for t, _ in tot), sum(u for _, u in tot)
+    if T >= 1 << 32 or N >= 1 << 32:
+        sys.exit("bench.py: a launch holds >= 2^32 reads of one sample (u32 offsets); lower --chunk")
+    rt = torch.empty(max(1, T), dtype=torch.int32, device=dev)
+    rn = torch.empty(max(1, N), dtype=torch.int32, device=dev)
+    so = bt = bn = 0
+    for (tid, first, n), (nt, nn) in zip(pieces, tot):   # pass 2: reads; then rebase the offsets
+        syn = pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=tid)
+        rc = lib.ss_synth_batch_device(ctx.h, C.byref(syn), first, n, ref.data_ptr() + so,
+                                       ot.data_ptr() + 4 * so, on.data_ptr() + 4 * so,
+                                       rt.data_ptr() + 4 * bt, rn.data_ptr() + 4 * bn, None, None)
+        if rc:
+            raise pkg.SniperError(rc, "ss_synth_batch_device")
+        if bt:
+            ot[so:so + n] += i32(bt)              # u32 offsets held in int32 tensors: wrap-around add
+        if bn:
+            on[so:so + n] += i32(bn)
+        so += n
+        bt += nt
+        bn += nn
+    ot[S] = i32(T)
+    on[S] = i32(N)
+    torch.cuda.synchronize(dev)
+    return {"ref": ref, "off_tumor": ot, "off_normal": on, "reads_tumor": rt, "reads_normal": rn,
+            "n_reads": (T, N), "n_sites": S}
 
 
 def main():
@@ -344,7 +414,8 @@ def main():
                          "shard: --sites synthetic sites per rank (weak scaling; the C2/C3/C5 depth runs)")
     ap.add_argument("--c4-scale", type=int, default=16,
                     help="C4 genome sites divided by this (3.09e9 / 16 = 1.93e8 sites: fits one GPU at N=1)")
-    ap.add_argument("--chunk", type=int, default=1 << 26, help="c4: most sites per launch")
+    ap.add_argument("--chunk", type=int, default=1 << 26,
+                    help="c4: most sites per launch (contig pieces packed back to back)")
     ap.add_argument("--sites", type=int, default=1 << 26, help="shard: sites per batch (per step, per GPU)")
     ap.add_argument("--batches", type=int, default=2, help="shard: distinct resident batches cycled per rank")
     ap.add_argument("--weak-sites", type=int, default=1 << 26,

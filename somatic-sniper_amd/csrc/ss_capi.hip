@@ -40,10 +40,10 @@ struct ss_ctx {
     /* model on the device */
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
-    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6] deep total */
+    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6] listed segments */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
-    uint32_t *d_deep_seg;     /* per-main-wave deep segment lengths */
+    uint32_t *d_deep_seg;     /* per-main-wave deep segment lengths, then the listed segment ids */
     /* timing: a pool of events, SS_EV_PER_LAUNCH per launch while enabled */
     int timing;
     std::vector<hipEvent_t> *ev;
@@ -189,7 +189,7 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
             }
     }
     TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t), hs));
-    TRY(dev_alloc((void **)&c->d_deep_seg, (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t), hs));
+    TRY(dev_alloc((void **)&c->d_deep_seg, 2 * (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t), hs));
     TRY(dev_alloc((void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t), hs));
 #undef TRY
     /* the tables, lists and counters are complete before any launch can use them */
@@ -267,7 +267,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     if (c->launched && s != c->last_stream) HIPCHK(hipStreamWaitEvent(s, c->done, 0));
     int rc = ensure_deep_cap(c, nseg * seg_cap, s);
     if (rc) return rc;
-    /* counters: deep2, deep total (err is sticky until ss_ctx_check) */
+    /* counters: deep2, listed segments (err is sticky until ss_ctx_check) */
     HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 2 * sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
@@ -286,12 +286,13 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.n_clamped = o->n_qadd_clamped;
     a.deep_list = c->d_deep_list;
     a.deep_seg_n = c->d_deep_seg;
+    a.deep_segs = c->d_deep_seg + (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64);
     a.deep_seg_cap = (uint32_t)seg_cap;
     a.deep_nseg = (uint32_t)nseg;
     a.deep_cap = c->deep_cap;
     a.deep2_list = c->d_deep_list + c->deep_cap;
     a.deep2_count = c->d_counters + 5;
-    a.deep_total = c->d_counters + 6;
+    a.deep_nsegs = c->d_counters + 6;
     a.err = c->d_counters + 2;
     a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;

@@ -64,8 +64,9 @@ struct ss_score_args {
     /* work lists (device; counters zeroed per launch) */
     uint32_t  *deep_list;     /* sites the main kernel's per-lane path does not score: one
                                  segment of deep_seg_cap entries per main-kernel wave, no atomics */
-    uint32_t  *deep_seg_n;    /* [deep_nseg] entries each main wave wrote (every wave writes) */
-    uint32_t  *deep_total;    /* sum of deep_seg_n (zeroed per launch): 0 lets the wide kernel exit at once */
+    uint32_t  *deep_seg_n;    /* [deep_nseg] entries each main wave wrote (written when nonzero) */
+    uint32_t  *deep_segs;     /* [deep_nseg] ids of the main waves that listed sites, compacted */
+    uint32_t  *deep_nsegs;    /* how many (zeroed per launch): the wide kernel walks only those */
     uint32_t   deep_seg_cap;
     uint32_t   deep_nseg;     /* = main-kernel waves */
     uint32_t   deep_cap;      /* deep2 list capacity (>= n_sites: cannot overflow) */

@@ -991,7 +991,7 @@ namespace {
 #define LN_N 128                     /* elements of the per-lane network          */
 #define LN_R (LN_N / 2)              /* its packed registers                      */
 #define LN_C (LN_N / 4)              /* 4-element chunks (one x4 load each)       */
-#define LN_G 4                       /* chunks loaded together                    */
+#define LN_P 4                       /* chunk loads in flight ahead of the key build */
 #define LN_WAVES (SS_MAIN_BLOCK / 64)
 
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -1072,75 +1072,147 @@ __device__ __forceinline__ uint32_t ln_rec(uint32_t k)
     return q | (k & 8u) << 3;
 }
 
-/* one pass of the key build: the lane's elements [0, na) are reads pa[0..na),
- * [na4, na4 + nb) reads pb[0..nb) (na4 = na rounded up to 4, so a chunk of 4
- * elements comes from one sample), every other element is a pad (0xffff).
- * sa / sb: the samples' key bits (0 tumor, 0x8000 normal).  Returns the
- * per-sample rms sums and group sizes (four 8-bit fields, base b at 8b) and
- * whether a contributing read has minq >= 64.  Every x4 load stays inside
- * the batch's reads (the caller routes a block that would pass their end to
- * the wide kernel). */
+/* Key-build lookup table (LDS, per workgroup): for a read's nt16 code and
+ * strand, the site's reference code and the sample, the ref-dependent part of
+ * its 16-bit order key (sample << 15 | base << 13 | hasbase << 4 |
+ * strand << 3; bam_nt16_nt4_table semantics, sniper_maqcns.c:19,153-154:
+ * single-base codes give their base with hasbase, '=' the reference's, any
+ * other code counts as A without hasbase) in the low half, and the read's
+ * one-hot group count increment in the high half: a nibble per base, base b
+ * at nibble LN_NIB[b] so that ln_nibbles_to_bytes moves it to byte b.
+ * Index: sample * 512 + ref16 * 32 + (nt16 | strand << 4). */
+#define LN_LUT (2 * 16 * 32 + 1)
+#define LN_LUT_NONC (2 * 16 * 32)    /* entry of a read with clamped q = 0: key 0xffff, no count */
+
+__device__ __forceinline__ void ln_lut_build(uint32_t *lut)
+{
+    for (uint32_t i = threadIdx.x; i < LN_LUT; i += blockDim.x) {
+        const uint32_t smp = i >> 9, ref16 = (i >> 5) & 15u, nt16 = i & 15u, st = (i >> 4) & 1u;
+        const uint32_t code = nt16 ? nt16 : ref16;
+        const uint32_t nt4 = code == 1u ? 0u : code == 2u ? 1u : code == 4u ? 2u : code == 8u ? 3u : 4u;
+        const uint32_t hb = nt4 < 4u ? 1u : 0u, base = hb ? nt4 : 0u;
+        const uint32_t nib = base == 0u ? 0u : base == 1u ? 2u : base == 2u ? 1u : 3u;
+        lut[i] = i == LN_LUT_NONC ? 0x0000ffffu
+                                  : (smp << 15 | base << 13 | hb << 4 | st << 3) | (1u << (4u * nib)) << 16;
+    }
+}
+
+/* four 4-bit counts (nibbles, see LN_LUT) -> four 8-bit counts, base b in byte b */
+__device__ __forceinline__ uint32_t ln_nibbles_to_bytes(uint32_t c)
+{
+    return (c & 0x0f0fu) | (c & 0xf0f0u) << 12;
+}
+
+/* one pass of the key build: the lane's elements [0, na) are reads
+ * ba[oa..oa+na), [na4, na4 + nb) reads bb[ob..ob+nb) (na4 = na rounded up to
+ * 4, so a chunk of 4 elements comes from one sample), every other element is
+ * a pad (0xffff).  la / lb: the samples' rows of the lookup table.  Returns
+ * the per-sample rms sums and group sizes (four 8-bit fields, base b at 8b)
+ * and the largest minq of any read (>= 64: the site needs 16-bit records).
+ * Every x4 load stays inside the batch's reads (the caller routes a block that
+ * would pass their end to the wide kernel); elements past a sample's reads are
+ * zeroed, which makes them non-contributing (key 0xffff, rms 0). */
 struct LaneIn {
     const uint32_t *ba, *bb;         /* wave-uniform array bases of A and B */
     uint32_t oa, ob;                 /* the lane's first read in A and in B */
-    uint32_t na, nb, na4, sa, sb;
-    uint32_t tb, th;                 /* read_key16 base tables of the site's ref */
+    uint32_t na, nb, na4;
+    uint32_t la, lb;                 /* LN_LUT row offsets of A and B (sample, ref16) */
+    const uint32_t *safe;            /* a readable x4 for chunks without reads */
 };
 
 struct LaneAcc {
     uint32_t rms_a, rms_b, cnt_a, cnt_b;
-    bool wild;
+    uint32_t maxq;
 };
 
-__device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, uint32_t nch, uint32_t cap, uint32_t (&v)[LN_R])
+/* the x4 load of chunk c (elements 4c .. 4c+3).  Unconditional: a chunk
+ * with no read of the lane loads the lane's first read of A instead (its
+ * words are zeroed by ln_chunk), so the load needs no branch and the ring of
+ * loads in flight stays in fixed registers. */
+__device__ __forceinline__ void ln_load(const LaneIn &in, uint32_t c, uint32_t (&x)[4])
 {
-    LaneAcc acc = {0u, 0u, 0u, 0u, false};
+    const uint32_t c4 = 4u * c;
+    const bool fa = c4 < in.na4;
+    const int lim = fa ? (int)in.na - (int)c4 : (int)(in.na4 + in.nb) - (int)c4;
+    const uint32_t *src = lim <= 0 ? in.safe : (fa ? in.ba + (in.oa + c4) : in.bb + (in.ob + (c4 - in.na4)));
+    const u32x4_a4 q4 = *reinterpret_cast<const u32x4_a4 *>(src);
+    x[0] = q4.x; x[1] = q4.y; x[2] = q4.z; x[3] = q4.w;
+}
+
+/* keys of chunk c from its loaded words x; rms / group sizes into acc */
+__device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint32_t *lut, uint32_t c, uint32_t cap,
+                                         const uint32_t (&x)[4], uint32_t (&v)[LN_R], LaneAcc &acc)
+{
+    const uint32_t c4 = 4u * c;
+    const bool fa = c4 < in.na4;
+    const int lim = fa ? (int)in.na - (int)c4 : (int)(in.na4 + in.nb) - (int)c4;
+    /* byte offset of the lookup row: a read indexes it by (nt16 | strand << 4) * 4;
+     * LN_LUT_NONC is the entry of a read with clamped q = 0 (key 0xffff, no count) */
+    const uint32_t row = (fa ? in.la : in.lb) * 4u;
+    uint32_t rd[4], minq[4], lo6[4], ent[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {                 /* the four table reads go out together */
+        rd[t] = t < lim ? x[t] : 0u;
+        minq[t] = min(rd[t] & 0xffu, (rd[t] >> 8) & 0xffu);
+        lo6[t] = rd[t] & 0x3f00u;
+        const bool nonc = (minq[t] | lo6[t]) == 0u;                /* clamped q = 0 (sniper_maqcns.c:165) */
+        const uint32_t off = nonc ? LN_LUT_NONC * 4u : (((rd[t] >> 14) & 0x7cu) | row);
+        ent[t] = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lut) + off);
+    }
+    uint32_t crms = 0, ccnt = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        acc.maxq = max(acc.maxq, minq[t]);
+        /* E = baseQ >> 6 at bit 1, nz = (baseQ & 0x3f) != 0 at bit 0 */
+        const uint32_t e1nz = ((rd[t] >> 13) & 6u) | (lo6[t] != 0u ? 1u : 0u);
+        const uint32_t key = ent[t] | minq[t] << 5 | e1nz;         /* low half; ent's high half: count */
+        ccnt += ent[t] >> 16;
+        const uint32_t tq = min(rd[t] & 0x7fu, cap);
+        crms += tq * tq;
+        const uint32_t e = c4 + (uint32_t)t;
+        if (e < LN_R) v[e] = key;                                   /* the high half: fixed later */
+        else v[LN_N - 1 - e] = __builtin_amdgcn_perm(~key, v[LN_N - 1 - e], 0x05040100u);
+    }
+    const uint32_t cb = ln_nibbles_to_bytes(ccnt);
+    acc.rms_a += fa ? crms : 0u;
+    acc.rms_b += fa ? 0u : crms;
+    acc.cnt_a += fa ? cb : 0u;
+    acc.cnt_b += fa ? 0u : cb;
+}
+
+__device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint32_t *lut, uint32_t nch, uint32_t cap,
+                                           uint32_t (&v)[LN_R])
+{
+    LaneAcc acc = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
     for (int r = 0; r < LN_R; ++r) v[r] = 0x0000ffffu;     /* pads: lo 0xffff, hi ~0xffff */
+    /* groups of LN_P chunks, two buffers: group g + 1 is loaded while group g
+     * is keyed (the loop unrolls fully: static buffer and v indices; skipped
+     * groups are wave-uniform) */
+    constexpr int NG = LN_C / LN_P;
+    uint32_t buf[2][LN_P][4];
+    if (nch > 0u) {
 #pragma unroll
-    for (int g = 0; g < LN_C / LN_G; ++g) {
-        if ((uint32_t)(g * LN_G) >= nch) continue;           /* wave-uniform; no break: the loop
-                                                                must unroll fully (static v indices) */
-        uint32_t x[LN_G][4];
-        int lim[LN_G];
-        bool fa[LN_G];
-#pragma unroll
-        for (int j = 0; j < LN_G; ++j) {
-            const uint32_t c4 = (uint32_t)(4 * (g * LN_G + j));
-            fa[j] = c4 < in.na4;
-            const uint32_t *src = fa[j] ? in.ba + (in.oa + c4) : in.bb + (in.ob + (c4 - in.na4));
-            lim[j] = fa[j] ? (int)in.na - (int)c4 : (int)(in.na4 + in.nb) - (int)c4;
-            u32x4_a4 q4 = {0u, 0u, 0u, 0u};
-            if (lim[j] > 0) q4 = *reinterpret_cast<const u32x4_a4 *>(src);
-            x[j][0] = q4.x; x[j][1] = q4.y; x[j][2] = q4.z; x[j][3] = q4.w;
-        }
-#pragma unroll
-        for (int j = 0; j < LN_G; ++j) {
-            const int c = g * LN_G + j;
-            const uint32_t sb = fa[j] ? in.sa : in.sb;
-            uint32_t crms = 0, ccnt = 0;
-            bool cwild = false;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const uint32_t rd = x[j][t];
-                const bool valid = t < lim[j];
-                uint32_t key = read_key16(rd, in.tb, in.th, sb);
-                key = valid ? key : 0xffffu;
-                cwild = cwild || (key != 0xffffu && (key & 0x1800u) != 0u);
-                const uint32_t tq = min(rd & 0x7fu, cap);
-                crms += valid ? tq * tq : 0u;
-                ccnt += key != 0xffffu ? 1u << ((key >> 10) & 0x18u) : 0u;
-                const int e = 4 * c + t;
-                if (e < LN_R) v[e] = key;                                     /* hi: a later chunk */
-                else v[LN_N - 1 - e] |= (key ^ 0xffffu) << 16;
-            }
-            acc.rms_a += fa[j] ? crms : 0u;
-            acc.rms_b += fa[j] ? 0u : crms;
-            acc.cnt_a += fa[j] ? ccnt : 0u;
-            acc.cnt_b += fa[j] ? 0u : ccnt;
-            acc.wild = acc.wild || cwild;
-        }
+        for (int j = 0; j < LN_P; ++j) ln_load(in, (uint32_t)j, buf[0][j]);
     }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if ((uint32_t)(g * LN_P) >= nch) continue;
+        if (g + 1 < NG && (uint32_t)((g + 1) * LN_P) < nch) {
+#pragma unroll
+            for (int j = 0; j < LN_P; ++j) ln_load(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
+        }
+#pragma unroll
+        for (int j = 0; j < LN_P; ++j) ln_chunk(in, lut, (uint32_t)(g * LN_P + j), cap, buf[g & 1][j], v, acc);
+    }
+    /* a low-half write left the element's count bits in the high half: for a
+     * register whose high element's chunk was never keyed, set the pad (0) */
+#pragma unroll
+    for (int r = 0; r < LN_R; r += 4)
+        if ((uint32_t)(LN_C - 1 - r / 4) >= nch && (uint32_t)(r / 4) < nch) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[r + k] &= 0xffffu;
+        }
     return acc;
 }
 
@@ -1258,8 +1330,10 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(3
 void ss_score_main(ss_score_args a)
 {
     __shared__ double fk[256];
+    __shared__ uint32_t lut[LN_LUT];
     __shared__ LaneLds LL[LN_WAVES];
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
+    ln_lut_build(lut);
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1291,32 +1365,31 @@ void ss_score_main(ss_score_args a)
         /* wave-uniform shape: joint when every ok site fits one network */
         /* a block whose x4 loads would pass the end of the batch's reads (its
          * last sites; one block per batch at most) goes to the wide kernel,
-         * which loads read by read */
-        if (__ballot(ok && (ot + nt4 > end_t || on + nn4 > end_n))) ok = false;
+         * which loads read by read; so does a batch of fewer than 4 tumor
+         * reads (the loads of read-less chunks go to reads_t[0..3]) */
+        if (__ballot(ok && (ot + nt4 > end_t || on + nn4 > end_n)) || end_t < 4u) ok = false;
         const bool joint = !__ballot(ok && nt4 + nn > LN_N);
-        uint32_t tb, th;
-        nt_tables(ref16, tb, th);
         bool wild = false;
         uint32_t lkN03 = 0, lkN47 = 0, lkN89 = 0, cnsN = 0, mqN = 0;
         /* joint: one pass, both samples; separate: the tumor, then the normal */
         for (uint32_t pass = 0; pass < (joint ? 1u : 2u); ++pass) {
             LaneIn in;
-            in.tb = tb;
-            in.th = th;
             const bool nrm = pass == 1u;
             in.ba = nrm ? a.reads_n : a.reads_t;
             in.oa = nrm ? on : ot;
             in.na = ok ? (nrm ? nn : nt) : 0u;
             in.na4 = ok ? (nrm ? nn4 : nt4) : 0u;
-            in.sa = nrm ? 0x8000u : 0u;
+            in.la = (nrm ? 512u : 0u) + ref16 * 32u;
             in.bb = a.reads_n;
             in.ob = on;
             in.nb = joint && ok ? nn : 0u;
-            in.sb = 0x8000u;
+            in.lb = 512u + ref16 * 32u;
+            in.safe = a.reads_t;          /* >= 4 readable words (a batch with fewer goes to the wide kernel) */
             const uint32_t nch = wave_max((in.na4 + in.nb + 3u) >> 2);
             uint32_t v[LN_R];
-            const LaneAcc acc = ln_keys(in, nch, cap, v);
-            wild = wild || acc.wild;
+            const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
+            /* a read of minq >= 64 needs 16-bit records: the wide kernel */
+            wild = wild || acc.maxq >= 64u;
             ln_levels<LN_R, 2>(v);
             ln_records(v, 4u * nch, L, lane);
             /* fold and finish the pass's samples: A (its records from 0), then
@@ -1368,9 +1441,9 @@ void ss_score_main(ss_score_args a)
         if (ok) decide_site(a, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
         wave_sync();
     }
-    if (lane == 0) {
+    if (lane == 0 && ndeep) {
         a.deep_seg_n[gw] = ndeep;
-        if (ndeep) atomicAdd(a.deep_total, ndeep);
+        a.deep_segs[atomicAdd(a.deep_nsegs, 1u)] = gw;
     }
 }
 
@@ -1597,7 +1670,8 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
 {
     __shared__ double fk[256];
     __shared__ WideLds L;
-    if (*a.deep_total == 0u) return;          /* the main kernel listed no site (every workgroup) */
+    const uint32_t nsegs = min(*a.deep_nsegs, a.deep_nseg);
+    if (nsegs == 0u) return;                 /* the main kernel listed no site (every workgroup) */
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -1608,9 +1682,10 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
-    /* the main kernel's per-wave segments, GB entries at a time */
-    for (uint32_t sg = blockIdx.x * WIDE_WAVES + wv; sg < a.deep_nseg; sg += gridDim.x * WIDE_WAVES)
-    for (uint32_t first = 0, scount = min(a.deep_seg_n[sg], a.deep_seg_cap); first < scount; first += GB) {
+    /* the listed segments of the main kernel's waves, GB entries at a time */
+    for (uint32_t si = blockIdx.x * WIDE_WAVES + wv; si < nsegs; si += gridDim.x * WIDE_WAVES)
+    for (uint32_t first = 0, sg = a.deep_segs[si], scount = min(a.deep_seg_n[sg], a.deep_seg_cap); first < scount;
+         first += GB) {
         const uint32_t *list = a.deep_list + (size_t)sg * a.deep_seg_cap;
         const uint32_t nlist = scount - first < GB ? scount - first : GB;
         /* site i's reads are in flight while site i-1 is sorted */

@@ -34,7 +34,8 @@ def test_bench_json_contract():
     assert abs(r["value"] - 2 * genome / (r["ms_per_step"] * 2e-3)) / r["value"] < 1e-3
     rf = r["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
-    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 and rf["launches_timed"] == 2 * 24
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert rf["launches_timed"] == 2 * r["ranks"][0]["launches_per_step"]
     import shutil
     if shutil.which("rocprofv3") or os.path.exists("/opt/rocm/bin/rocprofv3"):
         # live PMC passes: HBM traffic of the timed kernel and its VALU issue share
@@ -136,6 +137,37 @@ def test_bench_c4_ranks_self_spawned_gloo(gpus):
     assert abs(r["ms_per_step"] - worst) < 1e-3 + 1e-6 * worst
     assert abs(r["value"] - genome * 2 / (worst * 2 * 1e-3)) / r["value"] < 1e-3
     assert r["config"]["plan_imbalance"] < (1.01 if gpus == 8 else 1.001)
+
+
+@pytest.mark.gpu
+def test_c4_packed_launch_equals_its_pieces(pkg):
+    """bench.synth_pieces: contig pieces generated back to back in one HBM
+    batch (offsets rebased per piece) hold exactly the sites of each piece
+    (host generator, synth shard = contig), and score like them."""
+    import numpy as np
+    import torch
+    b = _bench()
+    dev = torch.device("cuda", 0)
+    args = type("A", (), dict(lt=60.0, ln=30.0, seed=0x5EED5A1DC0FFEE01))()
+    pieces = [(3, 1000, 700), (4, 0, 1234), (7, 55, 3)]
+    with pkg.Context(pkg.Params.default(), device=0) as ctx:
+        d = b.synth_pieces(ctx, pkg, args, pieces, dev)
+        host = [pkg.synth_batch_host(pkg.Synth.default(60, 30, seed=args.seed, shard=t), f, n) for t, f, n in pieces]
+        ref = np.concatenate([h.ref for h in host])
+        rt = np.concatenate([h.reads_tumor for h in host])
+        rn = np.concatenate([h.reads_normal for h in host])
+        ot = np.concatenate([[0]] + [h.off_tumor[1:] + sum(int(x.off_tumor[-1]) for x in host[:i])
+                                     for i, h in enumerate(host)]).astype(np.uint32)
+        on = np.concatenate([[0]] + [h.off_normal[1:] + sum(int(x.off_normal[-1]) for x in host[:i])
+                                     for i, h in enumerate(host)]).astype(np.uint32)
+        assert (d["ref"].cpu().numpy() == ref).all()
+        assert (d["off_tumor"].cpu().numpy().view(np.uint32) == ot).all()
+        assert (d["off_normal"].cpu().numpy().view(np.uint32) == on).all()
+        assert (d["reads_tumor"].cpu().numpy().view(np.uint32)[: len(rt)] == rt).all()
+        assert (d["reads_normal"].cpu().numpy().view(np.uint32)[: len(rn)] == rn).all()
+        s, _, _ = ctx.score_batch(pkg.Batch(ref, ot, on, rt, rn))
+        parts = np.concatenate([ctx.score_batch(h)[0] for h in host])
+        assert (s == parts).all()
 
 
 def test_c4_layout_partitions_the_genome():
