@@ -1118,6 +1118,7 @@ struct LaneIn {
     uint32_t na, nb, na4;
     uint32_t la, lb;                 /* LN_LUT row offsets of A and B (sample, ref16) */
     const uint32_t *safe;            /* a readable x4 for chunks without reads */
+    bool tail;                       /* wave-uniform: an x4 load could pass the end of the reads */
 };
 
 struct LaneAcc {
@@ -1126,15 +1127,25 @@ struct LaneAcc {
 };
 
 /* the x4 load of chunk c (elements 4c .. 4c+3).  Unconditional: a chunk
- * with no read of the lane loads the lane's first read of A instead (its
- * words are zeroed by ln_chunk), so the load needs no branch and the ring of
- * loads in flight stays in fixed registers. */
+ * with no read of the lane loads the batch's first reads instead (its words
+ * are zeroed by ln_chunk), so the load needs no branch and the ring of loads
+ * in flight stays in fixed registers.  In a tail block (the batch's last
+ * sites, whose last chunk could reach past the end of the reads, or a batch
+ * of fewer than 4 reads) the lane loads word by word, only its own reads. */
 __device__ __forceinline__ void ln_load(const LaneIn &in, uint32_t c, uint32_t (&x)[4])
 {
     const uint32_t c4 = 4u * c;
     const bool fa = c4 < in.na4;
     const int lim = fa ? (int)in.na - (int)c4 : (int)(in.na4 + in.nb) - (int)c4;
     const uint32_t *src = lim <= 0 ? in.safe : (fa ? in.ba + (in.oa + c4) : in.bb + (in.ob + (c4 - in.na4)));
+    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            x[t] = 0u;
+            if (t < lim) x[t] = src[t];
+        }
+        return;
+    }
     const u32x4_a4 q4 = *reinterpret_cast<const u32x4_a4 *>(src);
     x[0] = q4.x; x[1] = q4.y; x[2] = q4.z; x[3] = q4.w;
 }
@@ -1363,11 +1374,10 @@ void ss_score_main(ss_score_args a)
         bool ok = insite && formed && nt <= LN_N && nn <= LN_N;
         const uint32_t nt4 = (nt + 3u) & ~3u, nn4 = (nn + 3u) & ~3u;
         /* wave-uniform shape: joint when every ok site fits one network */
-        /* a block whose x4 loads would pass the end of the batch's reads (its
-         * last sites; one block per batch at most) goes to the wide kernel,
-         * which loads read by read; so does a batch of fewer than 4 tumor
-         * reads (the loads of read-less chunks go to reads_t[0..3]) */
-        if (__ballot(ok && (ot + nt4 > end_t || on + nn4 > end_n)) || end_t < 4u) ok = false;
+        /* a block whose x4 loads could pass the end of the batch's reads (its
+         * last sites) loads word by word; so does a batch of fewer than 4
+         * tumor reads (the x4 loads of read-less chunks go to reads_t[0..3]) */
+        const bool tail = __ballot(ok && (ot + nt4 > end_t || on + nn4 > end_n)) || end_t < 4u;
         const bool joint = !__ballot(ok && nt4 + nn > LN_N);
         bool wild = false;
         uint32_t lkN03 = 0, lkN47 = 0, lkN89 = 0, cnsN = 0, mqN = 0;
@@ -1384,7 +1394,8 @@ void ss_score_main(ss_score_args a)
             in.ob = on;
             in.nb = joint && ok ? nn : 0u;
             in.lb = 512u + ref16 * 32u;
-            in.safe = a.reads_t;          /* >= 4 readable words (a batch with fewer goes to the wide kernel) */
+            in.safe = a.reads_t;          /* >= 4 readable words unless tail */
+            in.tail = tail;
             const uint32_t nch = wave_max((in.na4 + in.nb + 3u) >> 2);
             uint32_t v[LN_R];
             const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
