@@ -998,7 +998,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 struct LaneLds {
     union {
-        uint32_t rec[LN_C][64];      /* fold record of element e, lane l: byte e & 3 of rec[e >> 2][l] */
+        /* fold record of element e, lane l: byte (e + 4) & 3 of rec[(e + 4) >> 2][l]; row 0 is a
+         * pad and row LN_C + 1 is never used, so a chain reads any 4-record window with two rows */
+        uint32_t rec[LN_C + 2][64];
         SlotRes res[64][2];          /* the two samples' results, for the decision */
     };
     uint32_t tres[5][64];            /* the tumor's results while the normal is sorted (registers) */
@@ -1138,6 +1140,10 @@ __device__ __forceinline__ void ln_load(const LaneIn &in, uint32_t c, uint32_t (
     const bool fa = c4 < in.na4;
     const int lim = fa ? (int)in.na - (int)c4 : (int)(in.na4 + in.nb) - (int)c4;
     const uint32_t *src = lim <= 0 ? in.safe : (fa ? in.ba + (in.oa + c4) : in.bb + (in.ob + (c4 - in.na4)));
+#ifdef SS_AB_NOLOAD
+    for (int t = 0; t < 4; ++t) x[t] = ((in.oa + c4 + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;
+    return;
+#endif
     if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -1235,30 +1241,44 @@ __device__ __forceinline__ void ln_records(const uint32_t (&v)[LN_R], uint32_t n
         if ((uint32_t)(4 * i) >= nel) continue;              /* wave-uniform */
         const uint32_t d = ln_rec(ln_elem(v, 4 * i)) | ln_rec(ln_elem(v, 4 * i + 1)) << 8 |
                            ln_rec(ln_elem(v, 4 * i + 2)) << 16 | ln_rec(ln_elem(v, 4 * i + 3)) << 24;
-        L.rec[i][lane] = d;
+        L.rec[i + 1][lane] = d;
     }
 }
 
 /* the ordered chain of one (sample, base) group: records [s0, s0 + n),
- * walked from the top (sniper_maqcns.c:162-172) */
+ * walked from the top (sniper_maqcns.c:162-172), four records per step: their
+ * window comes from two LDS rows (v_alignbyte), the four fk reads go out
+ * together and only the float accumulations stay serial.  Past the chain's
+ * end a read takes fk's zero entry (LN_FK_ZERO), which leaves e and f as they
+ * are (x + 0.0 == x), so lanes of shorter chains need no mask. */
+#define LN_FK_ZERO 256
 __device__ __forceinline__ void ln_chain(const LaneLds &L, uint32_t lane, uint32_t s0, uint32_t n,
                                          const double *fk, float &e, float &f)
 {
-    const uint8_t *col = reinterpret_cast<const uint8_t *>(&L.rec[0][0]) + 4u * lane;
+    const uint32_t *colw = &L.rec[0][lane];
+    const char *fkb = reinterpret_cast<const char *>(fk);
     e = 0.0f;
     f = 0.0f;
     uint32_t W = 0;                  /* strand 0 count in bits 0..15, strand 1 in 16..31 (units of 8 B) */
-    const char *fkb = reinterpret_cast<const char *>(fk);
-    for (uint32_t i = 0; __ballot(i < n); ++i) {
-        if (i < n) {
-            const uint32_t k = s0 + n - 1u - i;
-            const uint32_t r = col[(k >> 2) * 256u + (k & 3u)];
-            const uint32_t sh = (r >> 2) & 16u;                  /* strand << 4 */
-            const uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
+    for (uint32_t i = 0; __ballot(i < n); i += 4u) {
+        /* window of records k0 - 3 .. k0 (k0 = s0 + n - 1 - i) at column byte k0 + 1 */
+        const uint32_t b = i < n ? s0 + n - i : 4u;
+        const uint32_t row = (b >> 2) * 64u;
+        const uint32_t R = __builtin_amdgcn_alignbyte(colw[row + 64u], colw[row], b & 3u);
+        double t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t r = R >> (24 - 8 * j);                 /* record k0 - j in the low byte */
+            const uint32_t sh = (r >> 2) & 16u;                   /* strand << 4 */
+            const uint32_t w8 = i + (uint32_t)j < n ? __builtin_amdgcn_ubfe(W, sh, 16u) : 8u * LN_FK_ZERO;
             W += 8u << sh;
-            const double t = *reinterpret_cast<const double *>(fkb + w8);
-            e = (float)((double)e + t * (double)(r & 63u));
-            f = (float)((double)f + t);
+            t[j] = *reinterpret_cast<const double *>(fkb + w8);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t q = (R >> (24 - 8 * j)) & 63u;
+            e = (float)((double)e + t[j] * (double)q);
+            f = (float)((double)f + t[j]);
         }
     }
 }
@@ -1340,10 +1360,10 @@ __device__ __forceinline__ void ln_store_glf(ss_glf_t *dst, uint32_t ref16, uint
 __global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(3)))
 void ss_score_main(ss_score_args a)
 {
-    __shared__ double fk[256];
+    __shared__ double fk[LN_FK_ZERO + 1];
     __shared__ uint32_t lut[LN_LUT];
     __shared__ LaneLds LL[LN_WAVES];
-    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
+    for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < 256u ? ss_tab_fk(a.m)[i] : 0.0;
     ln_lut_build(lut);
     __syncthreads();
     const uint32_t lane = lane_id();
