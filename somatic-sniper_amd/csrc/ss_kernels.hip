@@ -1115,11 +1115,10 @@ __device__ __forceinline__ uint32_t ln_nibbles_to_bytes(uint32_t c)
  * would pass their end to the wide kernel); elements past a sample's reads are
  * zeroed, which makes them non-contributing (key 0xffff, rms 0). */
 struct LaneIn {
-    const uint32_t *ba, *bb;         /* wave-uniform array bases of A and B */
-    uint32_t oa, ob;                 /* the lane's first read in A and in B */
+    const uint32_t *pa, *pb;         /* element e's read: pa + e (e < na4), pb + e (e >= na4) */
     uint32_t na, nb, na4;
+    uint32_t nca, nab;               /* A's chunks (na4 / 4); na4 + nb */
     uint32_t la, lb;                 /* LN_LUT row offsets of A and B (sample, ref16) */
-    const uint32_t *safe;            /* a readable x4 for chunks without reads */
     bool tail;                       /* wave-uniform: an x4 load could pass the end of the reads */
 };
 
@@ -1128,23 +1127,23 @@ struct LaneAcc {
     uint32_t maxq;
 };
 
-/* the x4 load of chunk c (elements 4c .. 4c+3).  Unconditional: a chunk
- * with no read of the lane loads the batch's first reads instead (its words
- * are zeroed by ln_chunk), so the load needs no branch and the ring of loads
- * in flight stays in fixed registers.  In a tail block (the batch's last
- * sites, whose last chunk could reach past the end of the reads, or a batch
- * of fewer than 4 reads) the lane loads word by word, only its own reads. */
+/* the x4 load of chunk c (elements 4c .. 4c+3): A's reads below na4, then
+ * B's.  Unconditional: a chunk past the lane's reads loads whatever follows
+ * them in B's array (the caller makes sure that stays inside the batch's
+ * reads; ln_chunk zeroes the words), so the load needs no branch, its offset
+ * is the instruction's immediate and the loads in flight stay in fixed
+ * registers.  In a tail block (the batch's last sites, or a batch of fewer
+ * than 4 reads) the lane loads word by word, only its own reads. */
 __device__ __forceinline__ void ln_load(const LaneIn &in, uint32_t c, uint32_t (&x)[4])
 {
-    const uint32_t c4 = 4u * c;
-    const bool fa = c4 < in.na4;
-    const int lim = fa ? (int)in.na - (int)c4 : (int)(in.na4 + in.nb) - (int)c4;
-    const uint32_t *src = lim <= 0 ? in.safe : (fa ? in.ba + (in.oa + c4) : in.bb + (in.ob + (c4 - in.na4)));
+    const bool fa = c < in.nca;
+    const uint32_t *src = (fa ? in.pa : in.pb) + 4u * c;
 #ifdef SS_AB_NOLOAD
-    for (int t = 0; t < 4; ++t) x[t] = ((in.oa + c4 + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;
+    for (int t = 0; t < 4; ++t) x[t] = ((in.na + 4u * c + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;
     return;
 #endif
     if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */
+        const int lim = (int)(fa ? in.na : in.nab) - (int)(4u * c);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             x[t] = 0u;
@@ -1156,13 +1155,21 @@ __device__ __forceinline__ void ln_load(const LaneIn &in, uint32_t c, uint32_t (
     x[0] = q4.x; x[1] = q4.y; x[2] = q4.z; x[3] = q4.w;
 }
 
+/* (x != 0) as 0 / 1 in one VALU op (the compiler's form is a compare and a select) */
+__device__ __forceinline__ uint32_t ln_nz(uint32_t x)
+{
+    uint32_t r;
+    asm("v_min_u32 %0, 1, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 /* keys of chunk c from its loaded words x; rms / group sizes into acc */
 __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint32_t *lut, uint32_t c, uint32_t cap,
                                          const uint32_t (&x)[4], uint32_t (&v)[LN_R], LaneAcc &acc)
 {
     const uint32_t c4 = 4u * c;
-    const bool fa = c4 < in.na4;
-    const int lim = fa ? (int)in.na - (int)c4 : (int)(in.na4 + in.nb) - (int)c4;
+    const bool fa = c < in.nca;
+    const int lim = (int)(fa ? in.na : in.nab) - (int)c4;
     /* byte offset of the lookup row: a read indexes it by (nt16 | strand << 4) * 4;
      * LN_LUT_NONC is the entry of a read with clamped q = 0 (key 0xffff, no count) */
     const uint32_t row = (fa ? in.la : in.lb) * 4u;
@@ -1181,7 +1188,7 @@ __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint32_t *lut, 
     for (int t = 0; t < 4; ++t) {
         acc.maxq = max(acc.maxq, minq[t]);
         /* E = baseQ >> 6 at bit 1, nz = (baseQ & 0x3f) != 0 at bit 0 */
-        const uint32_t e1nz = ((rd[t] >> 13) & 6u) | (lo6[t] != 0u ? 1u : 0u);
+        const uint32_t e1nz = ((rd[t] >> 13) & 6u) | ln_nz(lo6[t]);
         const uint32_t key = ent[t] | minq[t] << 5 | e1nz;         /* low half; ent's high half: count */
         ccnt += ent[t] >> 16;
         const uint32_t tq = min(rd[t] & 0x7fu, cap);
@@ -1191,10 +1198,11 @@ __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint32_t *lut, 
         else v[LN_N - 1 - e] = __builtin_amdgcn_perm(~key, v[LN_N - 1 - e], 0x05040100u);
     }
     const uint32_t cb = ln_nibbles_to_bytes(ccnt);
-    acc.rms_a += fa ? crms : 0u;
-    acc.rms_b += fa ? 0u : crms;
+    /* totals and A's share (B's = total - A's); crms < 2^24 */
+    acc.rms_b += crms;
+    asm("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(acc.rms_a) : "v"(fa ? 1u : 0u), "v"(crms));
+    acc.cnt_b += cb;
     acc.cnt_a += fa ? cb : 0u;
-    acc.cnt_b += fa ? 0u : cb;
 }
 
 __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint32_t *lut, uint32_t nch, uint32_t cap,
@@ -1230,6 +1238,8 @@ __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint32_t *lut
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[r + k] &= 0xffffu;
         }
+    acc.rms_b -= acc.rms_a;          /* totals -> B's share */
+    acc.cnt_b -= acc.cnt_a;
     return acc;
 }
 
@@ -1375,7 +1385,6 @@ void ss_score_main(ss_score_args a)
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
     const uint32_t gw = blockIdx.x * LN_WAVES + wv;
-    uint32_t *seg = a.deep_list + (size_t)gw * a.deep_seg_cap;
     uint32_t ndeep = 0;
     for (uint32_t blk = gw; blk < nblocks; blk += nwaves) {
         const uint32_t s = blk * 64u + lane;
@@ -1405,18 +1414,19 @@ void ss_score_main(ss_score_args a)
         for (uint32_t pass = 0; pass < (joint ? 1u : 2u); ++pass) {
             LaneIn in;
             const bool nrm = pass == 1u;
-            in.ba = nrm ? a.reads_n : a.reads_t;
-            in.oa = nrm ? on : ot;
             in.na = ok ? (nrm ? nn : nt) : 0u;
             in.na4 = ok ? (nrm ? nn4 : nt4) : 0u;
-            in.la = (nrm ? 512u : 0u) + ref16 * 32u;
-            in.bb = a.reads_n;
-            in.ob = on;
             in.nb = joint && ok ? nn : 0u;
+            in.nca = in.na4 >> 2;
+            in.nab = in.na4 + in.nb;
+            const uint32_t ob = ok ? on : 0u;
+            in.pa = (nrm ? a.reads_n : a.reads_t) + (ok ? (nrm ? on : ot) : 0u);
+            in.pb = a.reads_n + ob - in.na4;
+            in.la = (nrm ? 512u : 0u) + ref16 * 32u;
             in.lb = 512u + ref16 * 32u;
-            in.safe = a.reads_t;          /* >= 4 readable words unless tail */
-            in.tail = tail;
-            const uint32_t nch = wave_max((in.na4 + in.nb + 3u) >> 2);
+            const uint32_t nch = wave_max((in.nab + 3u) >> 2);
+            /* chunks past A's reads load from pb: up to ob - na4 + 4 nch */
+            in.tail = tail || __ballot((uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4);
             uint32_t v[LN_R];
             const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
             /* a read of minq >= 64 needs 16-bit records: the wide kernel */
@@ -1449,8 +1459,9 @@ void ss_score_main(ss_score_args a)
         const uint64_t out = __ballot(insite && !ok);
         if (out) {
             if (insite && !ok) {
-                const uint32_t d = ndeep + (uint32_t)__popcll(out & ((1ull << lane) - 1ull));
-                if (d < a.deep_seg_cap) seg[d] = s;
+                const uint32_t d = ndeep + __builtin_amdgcn_mbcnt_hi((uint32_t)(out >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)out, 0u));
+                if (d < a.deep_seg_cap) a.deep_list[(size_t)gw * a.deep_seg_cap + d] = s;
                 else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
             }
             ndeep += (uint32_t)__popcll(out);

@@ -2,6 +2,7 @@
 # One rocprofv3 --pmc pass per argument (a space-separated counter list) over a
 # short shard-workload bench; per-kernel sums into gpurun_out/pmc/<i>.txt
 #   bash tools/pmc_probe.sh "SQC_ICACHE_HITS SQC_ICACHE_MISSES" "SQ_IFETCH"
+#   PMC_SITES=262144 PMC_ARGS="--lt 500 --ln 500" bash tools/pmc_probe.sh ...
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/pmc
@@ -12,7 +13,7 @@ i=0
 for ctrs in "$@"; do
   i=$((i + 1))
   timeout -s KILL 90 rocprofv3 --pmc $ctrs --output-format csv -d "$O/p$i" -o run -- \
-      python3 "$R/bench.py" --workload shard --no-cpu --no-pmc --steps 3 --warmup 1 --sites ${PMC_SITES:-4194304} \
+      python3 "$R/bench.py" --workload shard --no-cpu --no-pmc --steps 3 --warmup 1 --sites ${PMC_SITES:-4194304} ${PMC_ARGS:-} \
       > "$O/p$i.log" 2>&1 || { echo "pass $i ($ctrs) failed"; tail -5 "$O/p$i.log"; exit 1; }
   python3 - "$O/p$i" "$ctrs" > "$O/$i.txt" <<'PY'
 import csv, glob, sys, collections
