@@ -160,12 +160,12 @@ __device__ __forceinline__ float geno_p(int j, int k, const float es[4], const f
 template <int T0, int T1>
 __device__ __forceinline__ void geno_p_range(uint32_t role, const float es[4], const float fs[4],
                                              const uint32_t c[4], uint32_t tot, const ss_dev_model &m,
-                                             float out[5])
+                                             float *out)
 {
-    float ev[5];
-    uint32_t c2v[5];
-    bool homv[5];
-    double lhv[5], cfv[5];
+    float ev[T1];
+    uint32_t c2v[T1];
+    bool homv[T1];
+    double lhv[T1], cfv[T1];
 #pragma unroll
     for (int t = T0; t < T1; ++t) {
         int j, k;
@@ -1074,35 +1074,29 @@ __device__ __forceinline__ uint32_t ln_rec(uint32_t k)
     return q | (k & 8u) << 3;
 }
 
-/* Key-build lookup table (LDS, per workgroup): for a read's nt16 code and
- * strand, the site's reference code and the sample, the ref-dependent part of
- * its 16-bit order key (sample << 15 | base << 13 | hasbase << 4 |
- * strand << 3; bam_nt16_nt4_table semantics, sniper_maqcns.c:19,153-154:
- * single-base codes give their base with hasbase, '=' the reference's, any
- * other code counts as A without hasbase) in the low half, and the read's
- * one-hot group count increment in the high half: a nibble per base, base b
- * at nibble LN_NIB[b] so that ln_nibbles_to_bytes moves it to byte b.
- * Index: sample * 512 + ref16 * 32 + (nt16 | strand << 4). */
-#define LN_LUT (2 * 16 * 32 + 1)
-#define LN_LUT_NONC (2 * 16 * 32)    /* entry of a read with clamped q = 0: key 0xffff, no count */
+/* Key-build lookup table (LDS, per workgroup), 8-byte entries: for a read's
+ * nt16 code and strand, the site's reference code and the sample, .x the
+ * ref-dependent part of its 16-bit order key (sample << 15 | base << 13 |
+ * hasbase << 4 | strand << 3; bam_nt16_nt4_table semantics,
+ * sniper_maqcns.c:19,153-154: single-base codes give their base with hasbase,
+ * '=' the reference's, any other code counts as A without hasbase) and .y the
+ * read's group count increment (1 << 8 * base).  Entry 0 belongs to a
+ * non-contributing read (clamped q = 0, or a pad): key 0xffff, no count.  Row
+ * (sample, ref16) starts at byte 256 * (1 + sample * 16 + ref16) and a read
+ * indexes it by (nt16 | strand << 4) * 8 = (read >> 13) & 0xf8. */
+#define LN_LUT_BYTES (256 * (1 + 2 * 16))
 
-__device__ __forceinline__ void ln_lut_build(uint32_t *lut)
+__device__ __forceinline__ void ln_lut_build(uint2 *lut)
 {
-    for (uint32_t i = threadIdx.x; i < LN_LUT; i += blockDim.x) {
-        const uint32_t smp = i >> 9, ref16 = (i >> 5) & 15u, nt16 = i & 15u, st = (i >> 4) & 1u;
+    for (uint32_t i = threadIdx.x; i < LN_LUT_BYTES / 8u; i += blockDim.x) {
+        const uint32_t rw = i >> 5, smp = rw >= 17u ? 1u : 0u, ref16 = (rw - 1u) & 15u;
+        const uint32_t nt16 = i & 15u, st = (i >> 4) & 1u;
         const uint32_t code = nt16 ? nt16 : ref16;
         const uint32_t nt4 = code == 1u ? 0u : code == 2u ? 1u : code == 4u ? 2u : code == 8u ? 3u : 4u;
         const uint32_t hb = nt4 < 4u ? 1u : 0u, base = hb ? nt4 : 0u;
-        const uint32_t nib = base == 0u ? 0u : base == 1u ? 2u : base == 2u ? 1u : 3u;
-        lut[i] = i == LN_LUT_NONC ? 0x0000ffffu
-                                  : (smp << 15 | base << 13 | hb << 4 | st << 3) | (1u << (4u * nib)) << 16;
+        lut[i] = rw == 0u ? make_uint2(0xffffu, 0u)
+                          : make_uint2(smp << 15 | base << 13 | hb << 4 | st << 3, 1u << (8u * base));
     }
-}
-
-/* four 4-bit counts (nibbles, see LN_LUT) -> four 8-bit counts, base b in byte b */
-__device__ __forceinline__ uint32_t ln_nibbles_to_bytes(uint32_t c)
-{
-    return (c & 0x0f0fu) | (c & 0xf0f0u) << 12;
 }
 
 /* one pass of the key build: the lane's elements [0, na) are reads
@@ -1118,7 +1112,7 @@ struct LaneIn {
     const uint32_t *pa, *pb;         /* element e's read: pa + e (e < na4), pb + e (e >= na4) */
     uint32_t na, nb, na4;
     uint32_t nca, nab;               /* A's chunks (na4 / 4); na4 + nb */
-    uint32_t la, lb;                 /* LN_LUT row offsets of A and B (sample, ref16) */
+    uint32_t la, lb;                 /* byte offsets of A's and B's lookup rows (see LN_LUT_BYTES) */
     bool tail;                       /* wave-uniform: an x4 load could pass the end of the reads */
 };
 
@@ -1163,49 +1157,54 @@ __device__ __forceinline__ uint32_t ln_nz(uint32_t x)
     return r;
 }
 
-/* keys of chunk c from its loaded words x; rms / group sizes into acc */
-__device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint32_t *lut, uint32_t c, uint32_t cap,
+/* keys of chunk c from its loaded words x; rms / group sizes into acc.
+ * Elements past the sample's reads are masked to 0 (a non-contributing read);
+ * a non-contributing read's lookup offset is multiplied by 0 (entry 0). */
+__device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint2 *lut, uint32_t c, uint32_t cap,
                                          const uint32_t (&x)[4], uint32_t (&v)[LN_R], LaneAcc &acc)
 {
     const uint32_t c4 = 4u * c;
     const bool fa = c < in.nca;
     const int lim = (int)(fa ? in.na : in.nab) - (int)c4;
-    /* byte offset of the lookup row: a read indexes it by (nt16 | strand << 4) * 4;
-     * LN_LUT_NONC is the entry of a read with clamped q = 0 (key 0xffff, no count) */
-    const uint32_t row = (fa ? in.la : in.lb) * 4u;
-    uint32_t rd[4], minq[4], lo6[4], ent[4];
+    uint32_t valid, vl;                             /* bit t: element c4 + t is a read */
+    asm("v_med3_i32 %0, %1, 0, 4" : "=v"(vl) : "v"(lim));
+    asm("v_bfm_b32 %0, %1, 0" : "=v"(valid) : "v"(vl));
+    const uint32_t row = fa ? in.la : in.lb;
+    uint32_t rd[4], minq[4], lo6[4], y[4];
+    uint2 ent[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {                 /* the four table reads go out together */
-        rd[t] = t < lim ? x[t] : 0u;
+        uint32_t vm;                                /* 0 or ~0 (the compiler's form: compare + select) */
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(vm) : "v"(valid), "i"(t));
+        rd[t] = x[t] & vm;
         minq[t] = min(rd[t] & 0xffu, (rd[t] >> 8) & 0xffu);
         lo6[t] = rd[t] & 0x3f00u;
-        const bool nonc = (minq[t] | lo6[t]) == 0u;                /* clamped q = 0 (sniper_maqcns.c:165) */
-        const uint32_t off = nonc ? LN_LUT_NONC * 4u : (((rd[t] >> 14) & 0x7cu) | row);
-        ent[t] = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lut) + off);
+        y[t] = rd[t] >> 13;
+        /* contributing unless the clamped q is 0 (sniper_maqcns.c:165-167) */
+        const uint32_t off = __umul24((y[t] & 0xf8u) | row, ln_nz(minq[t] | lo6[t]));
+        ent[t] = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(lut) + off);
     }
     uint32_t crms = 0, ccnt = 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         acc.maxq = max(acc.maxq, minq[t]);
         /* E = baseQ >> 6 at bit 1, nz = (baseQ & 0x3f) != 0 at bit 0 */
-        const uint32_t e1nz = ((rd[t] >> 13) & 6u) | ln_nz(lo6[t]);
-        const uint32_t key = ent[t] | minq[t] << 5 | e1nz;         /* low half; ent's high half: count */
-        ccnt += ent[t] >> 16;
+        const uint32_t key = ent[t].x | minq[t] << 5 | (y[t] & 6u) | ln_nz(lo6[t]);   /* < 2^16 */
+        ccnt += ent[t].y;
         const uint32_t tq = min(rd[t] & 0x7fu, cap);
         crms += tq * tq;
         const uint32_t e = c4 + (uint32_t)t;
-        if (e < LN_R) v[e] = key;                                   /* the high half: fixed later */
-        else v[LN_N - 1 - e] = __builtin_amdgcn_perm(~key, v[LN_N - 1 - e], 0x05040100u);
+        if (e < LN_R) v[e] = key;                                   /* high half 0: a pad, see below */
+        else v[LN_N - 1 - e] |= (key ^ 0xffffu) << 16;
     }
-    const uint32_t cb = ln_nibbles_to_bytes(ccnt);
     /* totals and A's share (B's = total - A's); crms < 2^24 */
     acc.rms_b += crms;
     asm("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(acc.rms_a) : "v"(fa ? 1u : 0u), "v"(crms));
-    acc.cnt_b += cb;
-    acc.cnt_a += fa ? cb : 0u;
+    acc.cnt_b += ccnt;
+    acc.cnt_a += fa ? ccnt : 0u;
 }
 
-__device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint32_t *lut, uint32_t nch, uint32_t cap,
+__device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint2 *lut, uint32_t nch, uint32_t cap,
                                            uint32_t (&v)[LN_R])
 {
     LaneAcc acc = {0u, 0u, 0u, 0u, 0u};
@@ -1230,14 +1229,7 @@ __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint32_t *lut
 #pragma unroll
         for (int j = 0; j < LN_P; ++j) ln_chunk(in, lut, (uint32_t)(g * LN_P + j), cap, buf[g & 1][j], v, acc);
     }
-    /* a low-half write left the element's count bits in the high half: for a
-     * register whose high element's chunk was never keyed, set the pad (0) */
-#pragma unroll
-    for (int r = 0; r < LN_R; r += 4)
-        if ((uint32_t)(LN_C - 1 - r / 4) >= nch && (uint32_t)(r / 4) < nch) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[r + k] &= 0xffffu;
-        }
+    /* a high half never keyed stays 0: the complement of the pad key */
     acc.rms_b -= acc.rms_a;          /* totals -> B's share */
     acc.cnt_b -= acc.cnt_a;
     return acc;
@@ -1328,8 +1320,7 @@ __device__ __forceinline__ void ln_finish(const float es[4], const float fs[4], 
     uint32_t c[4];
     const uint32_t tot = rescale_counts(craw, c);
     float p[10];
-    geno_p5(0u, es, fs, c, tot, m, p);
-    geno_p5(1u, es, fs, c, tot, m, p + 5);
+    geno_p_range<0, 10>(0u, es, fs, c, tot, m, p);
     uint32_t lk[10], min_lk, rms_q;
     glf_finish(p, es, n, rms, m, lk, min_lk, rms_q, cns);
     lk03 = lk[0] | lk[1] << 8 | lk[2] << 16 | lk[3] << 24;
@@ -1371,7 +1362,7 @@ __global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(3
 void ss_score_main(ss_score_args a)
 {
     __shared__ double fk[LN_FK_ZERO + 1];
-    __shared__ uint32_t lut[LN_LUT];
+    __shared__ uint2 lut[LN_LUT_BYTES / 8];
     __shared__ LaneLds LL[LN_WAVES];
     for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < 256u ? ss_tab_fk(a.m)[i] : 0.0;
     ln_lut_build(lut);
@@ -1422,8 +1413,8 @@ void ss_score_main(ss_score_args a)
             const uint32_t ob = ok ? on : 0u;
             in.pa = (nrm ? a.reads_n : a.reads_t) + (ok ? (nrm ? on : ot) : 0u);
             in.pb = a.reads_n + ob - in.na4;
-            in.la = (nrm ? 512u : 0u) + ref16 * 32u;
-            in.lb = 512u + ref16 * 32u;
+            in.la = 256u * (1u + (nrm ? 16u : 0u) + ref16);
+            in.lb = 256u * (17u + ref16);
             const uint32_t nch = wave_max((in.nab + 3u) >> 2);
             /* chunks past A's reads load from pb: up to ob - na4 + 4 nch */
             in.tail = tail || __ballot((uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4);
@@ -1431,8 +1422,12 @@ void ss_score_main(ss_score_args a)
             const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
             /* a read of minq >= 64 needs 16-bit records: the wide kernel */
             wild = wild || acc.maxq >= 64u;
+#ifndef SS_AB_NONET                 /* SS_AB_*: phase ablations for timing (tools/ab.sh), never shipped */
             ln_levels<LN_R, 2>(v);
+#endif
+#ifndef SS_AB_NOREC
             ln_records(v, 4u * nch, L, lane);
+#endif
             /* fold and finish the pass's samples: A (its records from 0), then
              * in joint mode B (after A's contributing reads) */
             const uint32_t ca = acc.cnt_a;
@@ -1441,9 +1436,17 @@ void ss_score_main(ss_score_args a)
                 const bool smpN = nrm || k == 1u;
                 float es[4], fs[4];
                 uint32_t c[4];
+#ifndef SS_AB_NOFOLD
                 ln_fold(L, lane, k ? tot_a : 0u, k ? acc.cnt_b : acc.cnt_a, fk, es, fs, c);
+#else
+                for (int b = 0; b < 4; ++b) { es[b] = fs[b] = (float)(acc.cnt_a >> b); c[b] = (acc.cnt_a >> (8 * b)) & 0xffu; }
+#endif
                 uint32_t l03, l47, l89, cn, mq;
+#ifndef SS_AB_NOFIN
                 ln_finish(es, fs, c, smpN ? nn : nt, k ? acc.rms_b : acc.rms_a, a.m, l03, l47, l89, cn, mq);
+#else
+                l03 = __float_as_uint(es[0]); l47 = __float_as_uint(fs[1]); l89 = c[2]; cn = 0x11000000u; mq = c[3];
+#endif
                 if (smpN) {
                     lkN03 = l03; lkN47 = l47; lkN89 = l89; cnsN = cn; mqN = mq;
                 } else {
@@ -1480,7 +1483,11 @@ void ss_score_main(ss_score_args a)
             }
         }
         wave_sync();
+#ifndef SS_AB_NODECIDE
         if (ok) decide_site(a, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
+#else
+        if (ok) a.score[s] = (int)L.res[lane][0].cns;
+#endif
         wave_sync();
     }
     if (lane == 0 && ndeep) {
