@@ -88,6 +88,25 @@ __device__ __forceinline__ double cr_sqrt(double d)
     return s;
 }
 
+/* clamp_bar_e without the IEEE division in the common case: e / f <= 63 (e
+ * sums fk * q, f the same fk, q <= 63) and e * rcp(f) lies within a few ulp
+ * (< 2^-16) of the correctly rounded quotient, so floor(q + 0.5) is exact
+ * unless q + 0.5 falls within 2^-12 of an integer; those lanes (rare) take
+ * the exact division in a wave-uniform branch.  f = 0 (a genotype without
+ * other reads, whose index is unused) gives 4. */
+__device__ __forceinline__ int bar_e_fast(float e, float f)
+{
+    const float r = e * __builtin_amdgcn_rcpf(f) + 0.5f;
+    const float fr = __builtin_amdgcn_fractf(r);
+    const bool near = fr < 0x1p-12f || fr > 1.0f - 0x1p-12f;
+    int be = (int)__builtin_floorf(r);
+    if (__ballot(near)) {
+        if (near) be = (int)((double)(e / f) + 0.5);
+    }
+    be = be < 4 ? 4 : be;
+    return be > 63 ? 63 : be;
+}
+
 __device__ __forceinline__ int clamp_bar_e(float e, float f)
 {
     int be = (int)((double)(e / f) + 0.5);
@@ -170,18 +189,21 @@ __device__ __forceinline__ void geno_p_range(uint32_t role, const float es[4], c
     for (int t = T0; t < T1; ++t) {
         int j, k;
         geno_jk((int)role * 5 + t, j, k);
+        /* the reference's sums start at 0.0f: 0.0f + x == x for these x >= +0 */
         float e = 0.0f, f = 0.0f;
         uint32_t c2 = 0;
+        bool first = true;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const bool use = i != j && i != k;
-            e = use ? e + es[i] : e;
-            f = use ? f + fs[i] : f;
-            c2 += use ? c[i] : 0u;
+            if (i == j || i == k) continue;              /* compile-time */
+            e = first ? es[i] : e + es[i];
+            f = first ? fs[i] : f + fs[i];
+            c2 += c[i];
+            first = false;
         }
         const bool hom = j == k;
         const uint32_t il = hom ? 0u : (c[j] << 8 | c[k]);
-        const uint32_t ic = c2 ? ((uint32_t)clamp_bar_e(e, f) << 16 | tot << 8 | c2) : 0u;
+        const uint32_t ic = c2 ? ((uint32_t)bar_e_fast(e, f) << 16 | tot << 8 | c2) : 0u;
         lhv[t] = ss_tab_lhet(m)[il];
         cfv[t] = ss_tab_coef(m)[ic];
         ev[t] = e;
@@ -1254,6 +1276,7 @@ __device__ __forceinline__ void ln_records(const uint32_t (&v)[LN_R], uint32_t n
  * end a read takes fk's zero entry (LN_FK_ZERO), which leaves e and f as they
  * are (x + 0.0 == x), so lanes of shorter chains need no mask. */
 #define LN_FK_ZERO 256
+
 __device__ __forceinline__ void ln_chain(const LaneLds &L, uint32_t lane, uint32_t s0, uint32_t n,
                                          const double *fk, float &e, float &f)
 {
