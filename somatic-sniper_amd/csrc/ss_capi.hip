@@ -40,10 +40,11 @@ struct ss_ctx {
     /* model on the device */
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
-    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6] listed segments */
+    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6..7] listed
+                                 entries | segments << 32, [8] the wide kernel's chunk counter */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
-    uint32_t *d_deep_seg;     /* per-main-wave deep segment lengths, then the listed segment ids */
+    uint32_t *d_deep_seg;     /* listed segments' first entries, then their main-wave ids */
     /* timing: a pool of events, SS_EV_PER_LAUNCH per launch while enabled */
     int timing;
     std::vector<hipEvent_t> *ev;
@@ -267,8 +268,9 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     if (c->launched && s != c->last_stream) HIPCHK(hipStreamWaitEvent(s, c->done, 0));
     int rc = ensure_deep_cap(c, nseg * seg_cap, s);
     if (rc) return rc;
-    /* counters: deep2, listed segments (err is sticky until ss_ctx_check) */
-    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 2 * sizeof(uint32_t), s));
+    /* counters: deep2, listed segments and entries, the wide kernel's next
+     * chunk (err is sticky until ss_ctx_check) */
+    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 4 * sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
     memset(&a, 0, sizeof(a));
@@ -285,14 +287,15 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.glf = o->glf;
     a.n_clamped = o->n_qadd_clamped;
     a.deep_list = c->d_deep_list;
-    a.deep_seg_n = c->d_deep_seg;
+    a.deep_off = c->d_deep_seg;
     a.deep_segs = c->d_deep_seg + (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64);
     a.deep_seg_cap = (uint32_t)seg_cap;
     a.deep_nseg = (uint32_t)nseg;
     a.deep_cap = c->deep_cap;
     a.deep2_list = c->d_deep_list + c->deep_cap;
     a.deep2_count = c->d_counters + 5;
-    a.deep_nsegs = c->d_counters + 6;
+    a.deep_acc = reinterpret_cast<unsigned long long *>(c->d_counters + 6);   /* 8-byte aligned */
+    a.wide_next = c->d_counters + 8;
     a.err = c->d_counters + 2;
     a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;

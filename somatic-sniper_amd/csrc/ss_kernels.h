@@ -64,9 +64,10 @@ struct ss_score_args {
     /* work lists (device; counters zeroed per launch) */
     uint32_t  *deep_list;     /* sites the main kernel's per-lane path does not score: one
                                  segment of deep_seg_cap entries per main-kernel wave, no atomics */
-    uint32_t  *deep_seg_n;    /* [deep_nseg] entries each main wave wrote (written when nonzero) */
     uint32_t  *deep_segs;     /* [deep_nseg] ids of the main waves that listed sites, compacted */
-    uint32_t  *deep_nsegs;    /* how many (zeroed per launch): the wide kernel walks only those */
+    uint32_t  *deep_off;      /* [deep_nseg] their first entry in the listed order (ascending) */
+    unsigned long long *deep_acc; /* listed segments << 32 | listed entries (zeroed per launch) */
+    uint32_t  *wide_next;     /* the wide kernel's next chunk of GB listed entries (zeroed per launch) */
     uint32_t   deep_seg_cap;
     uint32_t   deep_nseg;     /* = main-kernel waves */
     uint32_t   deep_cap;      /* deep2 list capacity (>= n_sites: cannot overflow) */
@@ -84,7 +85,10 @@ struct ss_score_args {
 #define SS_MAIN_SITES      64    /* sites per main-kernel wave block           */
 #define SS_MAIN_GRID_PER_CU 128  /* main-kernel workgroups per CU: 4 resident, 32 rounds of short-lived waves (+5.5% over 16) */
 #define SS_DEEP_BLOCK      256
-#define SS_WIDE_BLOCK      512   /* 8 waves, one workgroup per CU (LDS)          */
+#ifndef SS_WIDE_BLOCK
+#define SS_WIDE_BLOCK      512   /* 8 waves, one workgroup per CU (LDS); 12 waves with a
+                                    smaller arena measured slower */
+#endif
 #define SS_WIDE_MAXSLOTS   2048  /* sort slots (tumor + pad + normal) per site    */
 
 /* Launchers (return hipError_t as int). */

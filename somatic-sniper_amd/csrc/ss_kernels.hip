@@ -928,7 +928,11 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         depth = m3.rec_n >> 16;
         rms = m3.rms;
         const RecT *rec = recs + (m3.rec_n & 0xffffu);
+#ifndef SS_AB_WNOFOLD
         fold_sample<RecT>(rec, cnt, fk, role, acc);
+#else
+        for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b] + (float)rec[b];
+#endif
     } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
@@ -946,7 +950,11 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     uint32_t c[4];
     const uint32_t tot = rescale_counts(cnt, c);
     float mine[5];
+#ifndef SS_AB_WNOFIN
     geno_p5(role, es, fs, c, tot, a.m, mine);
+#else
+    for (int t = 0; t < 5; ++t) mine[t] = es[t & 3] + (float)c[t & 3];
+#endif
 #pragma unroll
     for (int t = 0; t < 5; ++t) mine[t] = act ? mine[t] : 0.0f;
     float p[10];
@@ -1514,8 +1522,11 @@ void ss_score_main(ss_score_args a)
         wave_sync();
     }
     if (lane == 0 && ndeep) {
-        a.deep_seg_n[gw] = ndeep;
-        a.deep_segs[atomicAdd(a.deep_nsegs, 1u)] = gw;
+        /* one atomic numbers the segment and places its entries, so the
+         * offsets ascend with the segment index (the wide kernel searches them) */
+        const unsigned long long r = atomicAdd(a.deep_acc, 1ull << 32 | ndeep);
+        a.deep_segs[r >> 32] = gw;
+        a.deep_off[r >> 32] = (uint32_t)r;
     }
 }
 
@@ -1541,7 +1552,7 @@ void ss_score_main(ss_score_args a)
 namespace {
 
 #define WIDE_WAVES (SS_WIDE_BLOCK / 64)
-#define WIDE_LDS_REC 147456                /* u8 fold records per workgroup: 144 KB of LDS */
+#define WIDE_LDS_REC (WIDE_WAVES == 8 ? 147456 : 12064 * 12)   /* u8 fold records per workgroup: 141-144 KB */
 #define WIDE_ARENA (WIDE_LDS_REC / WIDE_WAVES)      /* per wave (< 2^16: Slot3 rec_n) */
 
 struct alignas(16) WideLds {
@@ -1610,8 +1621,13 @@ __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t i0 = i00 + (uint32_t)r * 64u;
+#ifndef SS_AB_WNOLOAD
             rd[2 * r] = i0 < lim ? __builtin_nontemporal_load(bp + i0) : 0u;
             rd[2 * r + 1] = i0 + 1u < lim ? __builtin_nontemporal_load(bp + i0 + 1) : 0u;
+#else
+            rd[2 * r] = i0 < lim ? ((i0 * 0x9E3779B1u) & 0x001f3f3fu) : 0u;
+            rd[2 * r + 1] = i0 + 1u < lim ? (((i0 + 1u) * 0x9E3779B1u) & 0x001f3f3fu) : 0u;
+#endif
         }
     } else {
         /* element e: tumor read e below sp, normal read e - sp above (a
@@ -1627,8 +1643,13 @@ __device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite
             const bool tum = e0 < sp;
             const uint32_t *src = (tum ? tp : np) + e0;
             const uint32_t lim = tum ? lt : ln;
+#ifndef SS_AB_WNOLOAD
             rd[2 * r] = e0 < lim ? __builtin_nontemporal_load(src) : 0u;
             rd[2 * r + 1] = e0 + 1u < lim ? __builtin_nontemporal_load(src + 1) : 0u;
+#else
+            rd[2 * r] = e0 < lim ? ((e0 * 0x9E3779B1u) & 0x001f3f3fu) : 0u;
+            rd[2 * r + 1] = e0 + 1u < lim ? (((e0 + 1u) * 0x9E3779B1u) & 0x001f3f3fu) : 0u;
+#endif
         }
     }
 }
@@ -1662,7 +1683,11 @@ __device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const Wi
         const bool tum = w.split ? lane < 32u : e0 < w.sp;
         const uint32_t rd0 = rd[2 * r], rd1 = rd[2 * r + 1];
         const uint32_t sb = tum ? 0u : 0x8000u;
+#ifndef SS_AB_WNOKEY
         const uint32_t k0 = read_key16(rd0, tb, th, sb), k1 = read_key16(rd1, tb, th, sb);
+#else
+        const uint32_t k0 = (rd0 & 0x7fffu) | sb, k1 = (rd1 & 0x7fffu) | sb;
+#endif
         const uint32_t t0 = min(rd0 & 0x7fu, cap), t1 = min(rd1 & 0x7fu, cap);
         const uint32_t x = t0 * t0 + t1 * t1;
         a_t += tum ? x : 0u;
@@ -1679,7 +1704,9 @@ __device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const Wi
         wn[i] = wave_sum(gc.n[i]);
     }
     if (SS_PRIO_WIDE) __builtin_amdgcn_s_setprio(SS_PRIO_WIDE);
+#ifndef SS_AB_WNOSORT
     packed_bitonic_flip<1, K>(v, !w.split);
+#endif
     if (SS_PRIO_WIDE) __builtin_amdgcn_s_setprio(0);
     const uint32_t c1 = GroupCount<K>::field(wt, 0), c2 = c1 + GroupCount<K>::field(wt, 1);
     const uint32_t c3 = c2 + GroupCount<K>::field(wt, 2), c4 = c3 + GroupCount<K>::field(wt, 3);
@@ -1691,6 +1718,11 @@ __device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const Wi
      * elements land past each sample's groups and are never read.  Lanes
      * wholly past the extent store nothing (the next site starts there). */
     const uint32_t nb = w.split ? 64u * K : c4;
+#ifdef SS_AB_WNOREC
+    if (lane == 0 && w.unit != 2u) { st2[0].rec_n = base | nt << 16; st2[0].cnt01 = c1; st2[0].cnt23 = c3; st2[0].rms = wave_sum(a_t); }
+    if (lane == 0 && w.unit != 1u) { st2[1].rec_n = (base + nb) | nn << 16; st2[1].cnt01 = c5; st2[1].cnt23 = c7; st2[1].rms = v[0][0]; }
+    return (int)(((w.split ? nb + (c8 - c4) : c8) + 31u) & ~31u);
+#endif
     /* extents stay multiples of 16 bytes: every unit's stores are 16-byte aligned */
     constexpr uint32_t XR = K < 8 ? 16u : 2u * K;
     const uint32_t extent = ((w.split ? nb + (c8 - c4) : c8) + XR - 1u) & ~(XR - 1u);
@@ -1742,7 +1774,8 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
 {
     __shared__ double fk[256];
     __shared__ WideLds L;
-    const uint32_t nsegs = min(*a.deep_nsegs, a.deep_nseg);
+    const unsigned long long acc = *a.deep_acc;
+    const uint32_t nsegs = min((uint32_t)(acc >> 32), a.deep_nseg), total = (uint32_t)acc;
     if (nsegs == 0u) return;                 /* the main kernel listed no site (every workgroup) */
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
     __syncthreads();
@@ -1754,21 +1787,33 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
-    /* the listed segments of the main kernel's waves, GB entries at a time */
-    for (uint32_t si = blockIdx.x * WIDE_WAVES + wv; si < nsegs; si += gridDim.x * WIDE_WAVES)
-    for (uint32_t first = 0, sg = a.deep_segs[si], scount = min(a.deep_seg_n[sg], a.deep_seg_cap); first < scount;
-         first += GB) {
-        const uint32_t *list = a.deep_list + (size_t)sg * a.deep_seg_cap;
-        const uint32_t nlist = scount - first < GB ? scount - first : GB;
-        /* site i's reads are in flight while site i-1 is sorted */
+    /* the listed entries (segments back to back in listing order), GB at a
+     * time, handed out by an atomic counter: waves that draw dense sites do
+     * fewer chunks */
+    for (;;) {
+        uint32_t ch = 0;
+        if (lane == 0u) ch = atomicAdd(a.wide_next, 1u);
+        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * GB;
+        if (first >= total) break;
+        const uint32_t nlist = total - first < GB ? total - first : GB;
+        /* the segment holding entry `first` (binary search over the ascending
+         * offsets, wave-uniform), then lane k steps to entry first + k's */
+        uint32_t lo = 0, hi = nsegs;
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.deep_off[mid] <= first) lo = mid;
+            else hi = mid;
+        }
         uint32_t i = 0, s_cur = 0;
         WideSite w_cur = {0, 0, 0, 0, 0, 0, 0, false, false};
-        uint32_t rd[32];
         /* the chunk's descriptors, lane k = entry k, loaded at once (one
          * exposed chain of dependent loads per chunk, not per site) */
         uint32_t c_s = 0, c_ot = 0, c_ot1 = 0, c_on = 0, c_on1 = 0, c_ref = 0;
         if (lane < nlist) {
-            c_s = list[first + lane];
+            const uint32_t p = first + lane;
+            uint32_t sg = lo;
+            while (sg + 1u < nsegs && a.deep_off[sg + 1u] <= p) ++sg;
+            c_s = a.deep_list[(size_t)a.deep_segs[sg] * a.deep_seg_cap + (p - a.deep_off[sg])];
             c_ot = a.off_t[c_s];
             c_ot1 = a.off_t[c_s + 1];
             c_on = a.off_n[c_s];
@@ -1785,10 +1830,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
             w.ref = rl(c_ref, k);
             wide_place(w, end_t, end_n);
         };
-        if (nlist) {
-            describe(0, s_cur, w_cur);
-            wide_load(a, w_cur, rd);
-        }
+        if (nlist) describe(0, s_cur, w_cur);
         uint32_t ext_t = 0;             /* arena bytes of the current site's tumor unit */
         bool dead = false;              /* that tumor unit sent the site to the deep list */
         while (i < nlist) {
@@ -1803,17 +1845,14 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 const uint32_t bound = w.unit ? ((w.nt + 31u) & ~31u) + ((w.nn + 31u) & ~31u)
                                               : ((w.split ? 32u * kb + w.nn : slots) + kb - 1u) & ~(kb - 1u);
                 if (w.unit != 2u && used + bound > WIDE_ARENA && !w.over) break;   /* next sub-group */
+                /* the unit's reads, loaded where it is sorted (the other waves
+                 * of the SIMD hide the latency) */
                 uint32_t cur[32];
-#pragma unroll
-                for (int k = 0; k < 32; ++k) cur[k] = rd[k];
+                wide_load(a, w, cur);
                 if (w.unit == 1u) {                       /* next: the same site's normal */
                     w_cur = wide_normal_unit(w);
-                    wide_load(a, w_cur, rd);
                 } else {
-                    if (i + 1 < nlist) {
-                        describe(i + 1, s_cur, w_cur);
-                        wide_load(a, w_cur, rd);
-                    }
+                    if (i + 1 < nlist) describe(i + 1, s_cur, w_cur);
                     ++i;
                 }
                 if (w.unit == 2u && dead) {               /* already on the deep list */
