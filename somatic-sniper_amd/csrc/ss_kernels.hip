@@ -1386,6 +1386,18 @@ __device__ __forceinline__ void ln_store_glf(ss_glf_t *dst, uint32_t ref16, uint
 
 }  // namespace
 
+/* The kernel's arguments re-read from the kernarg segment where they are
+ * used (the pointer is opaque to the compiler): the fields of the per-block
+ * tail (decision, glf stores, list appends) then do not stay live in SGPRs
+ * across the block loop, which spilled them to VGPR lanes. */
+__device__ __forceinline__ const ss_score_args &kernarg_args()
+{
+    typedef const __attribute__((address_space(4))) ss_score_args *kptr;
+    kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const ss_score_args *)p;
+}
+
 /* compiled for 3 waves per SIMD: the per-lane network's 64 registers, the
  * chunk loads in flight and the key arithmetic need about 160 VGPRs (at 128
  * the compiler spills); the records take 8 KB of LDS per wave */
@@ -1495,12 +1507,13 @@ void ss_score_main(ss_score_args a)
             if (insite && !ok) {
                 const uint32_t d = ndeep + __builtin_amdgcn_mbcnt_hi((uint32_t)(out >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)out, 0u));
-                if (d < a.deep_seg_cap) a.deep_list[(size_t)gw * a.deep_seg_cap + d] = s;
-                else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
+                const ss_score_args &k = kernarg_args();
+                if (d < k.deep_seg_cap) k.deep_list[(size_t)gw * k.deep_seg_cap + d] = s;
+                else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
             }
             ndeep += (uint32_t)__popcll(out);
         }
-        if (!formed && insite) atomicOr(a.err, SS_KERR_MALFORMED);
+        if (!formed && insite) atomicOr(kernarg_args().err, SS_KERR_MALFORMED);
         const uint32_t dt = nt > 16777215u ? 16777215u : nt, dn = nn > 16777215u ? 16777215u : nn;
         const uint32_t lkT03 = L.tres[0][lane], lkT47 = L.tres[1][lane], lkT89 = L.tres[2][lane];
         const uint32_t cnsT = L.tres[3][lane], mqT = L.tres[4][lane];
@@ -1508,14 +1521,15 @@ void ss_score_main(ss_score_args a)
         if (ok) {
             ln_store_res(L.res[lane][0], lkT03, lkT47, lkT89, cnsT, dt, mqT);
             ln_store_res(L.res[lane][1], lkN03, lkN47, lkN89, cnsN, dn, mqN);
-            if (a.glf) {
-                ln_store_glf(&a.glf[2ull * s], ref16, lkT03, lkT47, lkT89, mqT, dt);
-                ln_store_glf(&a.glf[2ull * s + 1], ref16, lkN03, lkN47, lkN89, mqN, dn);
+            ss_glf_t *glf = kernarg_args().glf;
+            if (glf) {
+                ln_store_glf(&glf[2ull * s], ref16, lkT03, lkT47, lkT89, mqT, dt);
+                ln_store_glf(&glf[2ull * s + 1], ref16, lkN03, lkN47, lkN89, mqN, dn);
             }
         }
         wave_sync();
 #ifndef SS_AB_NODECIDE
-        if (ok) decide_site(a, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
+        if (ok) decide_site(kernarg_args(), s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
 #else
         if (ok) a.score[s] = (int)L.res[lane][0].cns;
 #endif
@@ -1524,9 +1538,10 @@ void ss_score_main(ss_score_args a)
     if (lane == 0 && ndeep) {
         /* one atomic numbers the segment and places its entries, so the
          * offsets ascend with the segment index (the wide kernel searches them) */
-        const unsigned long long r = atomicAdd(a.deep_acc, 1ull << 32 | ndeep);
-        a.deep_segs[r >> 32] = gw;
-        a.deep_off[r >> 32] = (uint32_t)r;
+        const ss_score_args &k = kernarg_args();
+        const unsigned long long r = atomicAdd(k.deep_acc, 1ull << 32 | ndeep);
+        k.deep_segs[r >> 32] = gw;
+        k.deep_off[r >> 32] = (uint32_t)r;
     }
 }
 
@@ -1798,10 +1813,11 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
         const uint32_t nlist = total - first < GB ? total - first : GB;
         /* the segment holding entry `first` (binary search over the ascending
          * offsets, wave-uniform), then lane k steps to entry first + k's */
+        const ss_score_args &k = kernarg_args();
         uint32_t lo = 0, hi = nsegs;
         while (hi - lo > 1u) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (a.deep_off[mid] <= first) lo = mid;
+            if (k.deep_off[mid] <= first) lo = mid;
             else hi = mid;
         }
         uint32_t i = 0, s_cur = 0;
@@ -1812,14 +1828,14 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
         if (lane < nlist) {
             const uint32_t p = first + lane;
             uint32_t sg = lo;
-            while (sg + 1u < nsegs && a.deep_off[sg + 1u] <= p) ++sg;
-            c_s = a.deep_list[(size_t)a.deep_segs[sg] * a.deep_seg_cap + (p - a.deep_off[sg])];
-            c_ot = a.off_t[c_s];
-            c_ot1 = a.off_t[c_s + 1];
-            c_on = a.off_n[c_s];
-            c_on1 = a.off_n[c_s + 1];
-            const uint32_t rc = a.ref[c_s];
-            c_ref = rc | (uint32_t)ss_tab_nt16(a.m)[rc] << 8;
+            while (sg + 1u < nsegs && k.deep_off[sg + 1u] <= p) ++sg;
+            c_s = k.deep_list[(size_t)k.deep_segs[sg] * k.deep_seg_cap + (p - k.deep_off[sg])];
+            c_ot = k.off_t[c_s];
+            c_ot1 = k.off_t[c_s + 1];
+            c_on = k.off_n[c_s];
+            c_on1 = k.off_n[c_s + 1];
+            const uint32_t rc = k.ref[c_s];
+            c_ref = rc | (uint32_t)ss_tab_nt16(k.m)[rc] << 8;
         }
         auto describe = [&](uint32_t k, uint32_t &s, WideSite &w) {
             s = rl(c_s, k);
@@ -1848,7 +1864,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 /* the unit's reads, loaded where it is sorted (the other waves
                  * of the SIMD hide the latency) */
                 uint32_t cur[32];
-                wide_load(a, w, cur);
+                wide_load(kernarg_args(), w, cur);
                 if (w.unit == 1u) {                       /* next: the same site's normal */
                     w_cur = wide_normal_unit(w);
                 } else {
@@ -1867,9 +1883,10 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                                                : sort_site_wide<16>(cur, w, ref16, cap, arena, base, slot + 2 * G);
                 if (ext < 0) {
                     if (lane == 0) {
-                        const uint32_t d = atomicAdd(a.deep2_count, 1u);
-                        if (d < a.deep_cap) a.deep2_list[d] = s;
-                        else atomicOr(a.err, SS_KERR_DEEP_OVERFLOW);
+                        const ss_score_args &k = kernarg_args();
+                        const uint32_t d = atomicAdd(k.deep2_count, 1u);
+                        if (d < k.deep_cap) k.deep2_list[d] = s;
+                        else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
                     }
                     dead = w.unit == 1u;
                     continue;
@@ -1886,7 +1903,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
                 ++G;
             }
             wave_sync();
-            if (G) finish_sub<uint8_t>(a, G, arena, slot, res, sites, refcs, fk);
+            if (G) finish_sub<uint8_t>(kernarg_args(), G, arena, slot, res, sites, refcs, fk);
         }
     }
 }
