@@ -34,6 +34,7 @@ struct bgzf_reader {
     slot_t *one;
     void *dec;
     int eof;
+    int64_t coff_cur, coff_next;   /* file offsets of the current member and the next one */
     /* threaded mode */
     slot_t *slots;
     slot_t *cur;          /* the slot the consumer is draining (it owns it: no lock) */
@@ -205,13 +206,15 @@ static void *worker_main(void *arg)
     return NULL;
 }
 
-bgzf_reader_t *bgzf_open(const char *path, int n_threads)
+static bgzf_reader_t *open_common(const char *path, int n_threads, int64_t coff)
 {
     bgzf_reader_t *r = (bgzf_reader_t *)calloc(1, sizeof *r);
     if (!r) return NULL;
     if (strcmp(path, "-") == 0) r->fp = stdin;
     else { r->fp = fopen(path, "rb"); r->own_fp = 1; }
     if (!r->fp) { free(r); return NULL; }
+    if (coff > 0 && fseeko(r->fp, (off_t)coff, SEEK_SET) != 0) { fclose(r->fp); free(r); return NULL; }
+    r->coff_cur = r->coff_next = coff;
     r->n_threads = n_threads;
     if (n_threads <= 0) {
         r->one = (slot_t *)calloc(1, sizeof(slot_t));
@@ -232,6 +235,27 @@ bgzf_reader_t *bgzf_open(const char *path, int n_threads)
     return r;
 }
 
+bgzf_reader_t *bgzf_open(const char *path, int n_threads) { return open_common(path, n_threads, 0); }
+
+bgzf_reader_t *bgzf_open_at(const char *path, int n_threads, uint64_t voff)
+{
+    if (strcmp(path, "-") == 0) return NULL;
+    bgzf_reader_t *r = open_common(path, n_threads, (int64_t)(voff >> 16));
+    if (!r) return NULL;
+    uint8_t skip[65536];
+    const size_t k = (size_t)(voff & 0xffffu);
+    if (k && bgzf_read(r, skip, k) != (long)k) { bgzf_close(r); return NULL; }
+    return r;
+}
+
+int64_t bgzf_tell(const bgzf_reader_t *r)
+{
+    if (r->slots) return -1;
+    const slot_t *s = r->one;
+    if (s->state != SLOT_DONE || s->pos == s->ulen) return r->coff_next << 16;
+    return r->coff_cur << 16 | (int64_t)s->pos;
+}
+
 long bgzf_read(bgzf_reader_t *r, void *dst, size_t n)
 {
     uint8_t *out = (uint8_t *)dst;
@@ -241,6 +265,7 @@ long bgzf_read(bgzf_reader_t *r, void *dst, size_t n)
         while (done < n) {
             if (s->state != SLOT_DONE || s->pos == s->ulen) {
                 if (r->eof) break;
+                const int64_t at = r->coff_next;
                 const int rc = read_member(r->fp, s, r->err);
                 if (rc == 0) { r->eof = 1; break; }
                 if (rc < 0 || inflate_member(s, r->dec)) {
@@ -248,6 +273,8 @@ long bgzf_read(bgzf_reader_t *r, void *dst, size_t n)
                     return -1;
                 }
                 s->state = SLOT_DONE;
+                r->coff_cur = at;
+                r->coff_next = (int64_t)ftello(r->fp);
                 continue;
             }
             size_t k = s->ulen - s->pos;

@@ -59,6 +59,7 @@ typedef struct {
 
 struct col_stream {
     bgzf_reader_t *fp;
+    col_seed_t seed;
     uint32_t flag_mask;
     int mapq_thresh;
     int error;
@@ -363,8 +364,13 @@ static void *reader_main(void *arg)
     int32_t T = 0, max_tid = -1;     /* the walk's contig */
     int64_t W = 0;                   /* the walk's position at the next load */
     int64_t lo = 0;                  /* windows of T before lo are queued */
+    if (S->seed.has_prev) {          /* the state right after the last record loaded before the range */
+        T = max_tid = S->seed.prev_tid;
+        W = S->seed.prev_pos > 0 ? S->seed.prev_pos : 0;
+    }
     int rc;
     while ((rc = bam_record_read(S->fp, &rec)) > 0) {
+        if (rec.tid >= S->seed.stop_tid) break;            /* the next range's first record */
         if ((rec.flag & S->flag_mask) || rec.mapq < S->mapq_thresh) continue;
         if (rec.tid < max_tid) {
             fprintf(stderr, "[bam_pileup_core] the input is not sorted. Abort!\n");
@@ -418,9 +424,16 @@ out:
 
 col_stream_t *col_stream_start(bgzf_reader_t *fp, int mask, int thresh, int n_workers)
 {
+    const col_seed_t whole = {0, 0, 0, INT32_MAX};
+    return col_stream_start_at(fp, mask, thresh, n_workers, &whole);
+}
+
+col_stream_t *col_stream_start_at(bgzf_reader_t *fp, int mask, int thresh, int n_workers, const col_seed_t *seed)
+{
     col_stream_t *S = (col_stream_t *)calloc(1, sizeof *S);
     if (!S) return NULL;
     S->fp = fp;
+    S->seed = *seed;
     S->flag_mask = mask < 0 ? SS_BAM_DEF_MASK : (SS_BAM_FUNMAP | (uint32_t)mask);
     S->mapq_thresh = thresh < 0 ? 0 : thresh;
     S->n_workers = n_workers < 1 ? 1 : (n_workers > MAX_WORKERS ? MAX_WORKERS : n_workers);

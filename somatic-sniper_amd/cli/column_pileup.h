@@ -35,6 +35,20 @@ typedef struct col_stream col_stream_t;
 /* Starts the reader thread over fp (header already read) and n_workers
  * window-building threads.  mask / thresh as in dual_pileup_run. */
 col_stream_t *col_stream_start(bgzf_reader_t *fp, int mask, int thresh, int n_workers);
+
+/* A stream over one range of contigs (the contig-parallel pileup): fp is
+ * positioned at the range's first record; the walk state is what the whole
+ * file's walk has there -- by the rules above it depends only on the last
+ * record loaded before it (its contig becomes the walk's contig and its
+ * position W) -- and the stream ends at the first record of contig
+ * stop_tid. */
+typedef struct {
+    int has_prev;            /* 0: the range starts the file (walk at contig 0, W = 0) */
+    int32_t prev_tid;
+    int64_t prev_pos;
+    int32_t stop_tid;        /* INT32_MAX: to the end of the file */
+} col_seed_t;
+col_stream_t *col_stream_start_at(bgzf_reader_t *fp, int mask, int thresh, int n_workers, const col_seed_t *seed);
 /* Next reported column: 1 with its contig, position, raw entry count r and
  * the np packed non-deleted entries (valid until the next call); 0 at the
  * end of the stream. */

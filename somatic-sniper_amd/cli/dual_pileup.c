@@ -321,12 +321,13 @@ static int stream_next(stream_t *S, int32_t *tid, int32_t *pos, const uint32_t *
  * positions both walks report with entries: a walk that moves to a later
  * contig has no entries left on the earlier one, so the positions it skips
  * the other walk through are never shared. */
-static int column_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, dual_site_fn fn,
-                      void *data)
+static int column_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, const col_seed_t *s1,
+                      const col_seed_t *s2, dual_site_fn fn, void *data)
 {
     const char *ew = getenv("SS_PILEUP_WORKERS");
     const int nw = ew && *ew ? atoi(ew) : 3;                 /* window builders per sample */
-    col_stream_t *a = col_stream_start(fp1, mask, thresh, nw), *b = col_stream_start(fp2, mask, thresh, nw);
+    col_stream_t *a = col_stream_start_at(fp1, mask, thresh, nw, s1);
+    col_stream_t *b = col_stream_start_at(fp2, mask, thresh, nw, s2);
     if (!a || !b) { fprintf(stderr, "out of memory\n"); exit(1); }
     int32_t t1, p1, t2, p2;
     int r1, r2, np1, np2;
@@ -355,7 +356,10 @@ static int column_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thre
 int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, int threaded,
                     dual_site_fn fn, void *data)
 {
-    if (threaded == 2) return column_run(fp1, fp2, mask, thresh, fn, data);
+    if (threaded == 2) {
+        const col_seed_t whole = {0, 0, 0, INT32_MAX};
+        return column_run(fp1, fp2, mask, thresh, &whole, &whole, fn, data);
+    }
     walker_t *w1 = (walker_t *)malloc(sizeof(walker_t)), *w2 = (walker_t *)malloc(sizeof(walker_t));
     if (!w1 || !w2) { free(w1); free(w2); return -1; }
     walker_init(w1, fp1, mask, thresh);
@@ -437,4 +441,10 @@ int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh
     free(w1);
     free(w2);
     return err ? -1 : 0;
+}
+
+int dual_pileup_range(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, const col_seed_t *s1,
+                      const col_seed_t *s2, dual_site_fn fn, void *data)
+{
+    return column_run(fp1, fp2, mask, thresh, s1, s2, fn, data);
 }

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "bam_reader.h"
+#include "column_pileup.h"
 
 typedef struct {
     const bam_record_t *b;
@@ -41,5 +42,14 @@ typedef int (*dual_site_fn)(int32_t tid, int32_t pos, int n1, int n2, const uint
  * or -1 on a read error (message on stderr). */
 int dual_pileup_run(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, int threaded,
                     dual_site_fn fn, void *data);
+
+/* Column mode over one contig range of both files (the contig-parallel
+ * pileup, sniper_cli.c): fp1 / fp2 positioned at the range's first records,
+ * s1 / s2 the walks' states there (column_pileup.h).  The sites reported are
+ * those of the whole-file walk on the range's contigs: both walks' states
+ * depend only on their own files, and the lockstep loop reports exactly the
+ * positions both walks report with entries (column_run). */
+int dual_pileup_range(bgzf_reader_t *fp1, bgzf_reader_t *fp2, int mask, int thresh, const col_seed_t *s1,
+                      const col_seed_t *s2, dual_site_fn fn, void *data);
 
 #endif

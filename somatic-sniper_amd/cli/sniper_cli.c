@@ -18,8 +18,16 @@
  * consecutive batches to whichever device's scorer is free; outputs are
  * written strictly in batch order, so the file is identical for any number
  * of devices ("one streaming pileup per BAM feeding all
- * GPUs" -- the reference does not require indexed BAMs, so a contig-sharded
- * pileup could not seek).
+ * GPUs").
+ *
+ * Contig groups: when both BAMs have an index (.bai; the reference does not
+ * need one, so this is optional), the contigs are cut into SS_CONTIG_GROUPS
+ * (default 4) ranges of about equal compressed size, and each range runs its
+ * own pileup (both files read from the range's first records, bam_index.h),
+ * batches and scorers; the ranges' outputs are concatenated in contig order.
+ * Each walk's state at a range start is seeded from the last record its file
+ * loads before the range (column_pileup.h), so the sites, entries and output
+ * bytes are those of the single streaming walk.
  *
  * A site is what glf_somatic (somatic_sniper.c:109) sees: the ref char of
  * the cached contig (fai fetch, :112-117) and the non-deleted, mapped reads of
@@ -35,7 +43,9 @@
  * SS_DUMP_PILEUP=FILE (test hook: also write every reported site, see
  * dump_site()), SS_PILEUP_ONLY=1 (test / timing hook: walk (and dump) without
  * scoring, so the pileup restatement is testable on a host without a GPU; no
- * output records are written), SS_TIMING=1 (phase times on stderr).
+ * output records are written), SS_TIMING=1 (phase times on stderr),
+ * SS_CONTIG_GROUPS (contig ranges pileup in parallel when both BAMs are
+ * indexed, default 4; 1 keeps the single streaming walk).
  */
 #include <getopt.h>
 #include <time.h>
@@ -45,6 +55,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include "bam_index.h"
 #include "bam_reader.h"
 #include "bgzf_reader.h"
 #include "dual_pileup.h"
@@ -390,6 +401,167 @@ static int parse_devices(const char *s, int *dev, int *n)
     }
 }
 
+/* ---- contig groups (indexed BAMs) ------------------------------------------ */
+typedef struct {
+    run_t R;
+    const char *bam1, *bam2;
+    int32_t t0, t1;           /* contigs [t0, t1) */
+    uint64_t v1, v2;          /* the files' first records at or after t0 (UINT64_MAX: none) */
+    col_seed_t s1, s2;
+    int mapq, bthreads;
+    char *obuf, *dbuf;        /* the group's output / dump, concatenated in group order */
+    size_t olen, dlen;
+    scorer_arg_t sarg[MAX_DEV];
+    int err;
+} group_t;
+
+static void run_scorers_start(run_t *R, scorer_arg_t *sarg)
+{
+    for (int k = 0; k < R->n_dev; ++k) {
+        sarg[k].R = R;
+        sarg[k].k = k;
+        pthread_create(&R->th[k], NULL, scorer_main, &sarg[k]);
+    }
+}
+
+static void run_scorers_finish(run_t *R)
+{
+    if (filling(R)->n) submit(R);
+    pthread_mutex_lock(&R->mu);
+    R->quit = 1;
+    pthread_cond_broadcast(&R->cv);
+    pthread_mutex_unlock(&R->mu);
+    for (int k = 0; k < R->n_dev; ++k) pthread_join(R->th[k], NULL);
+}
+
+static void *group_main(void *arg)
+{
+    group_t *g = (group_t *)arg;
+    run_t *R = &g->R;
+    run_scorers_start(R, g->sarg);
+    if (g->v1 != UINT64_MAX && g->v2 != UINT64_MAX) {   /* a file without records here: no shared site */
+        bgzf_reader_t *f1 = bgzf_open_at(g->bam1, g->bthreads, g->v1);
+        bgzf_reader_t *f2 = bgzf_open_at(g->bam2, g->bthreads, g->v2);
+        if (!f1 || !f2) {
+            fprintf(stderr, "[bam-somaticsniper] cannot seek in the indexed BAMs\n");
+            g->err = 1;
+        } else if (dual_pileup_range(f1, f2, (int)SS_BAM_DEF_MASK, g->mapq, &g->s1, &g->s2, on_site, R)) {
+            g->err = 1;
+        }
+        if (f1) bgzf_close(f1);
+        if (f2) bgzf_close(f2);
+    }
+    run_scorers_finish(R);
+    return NULL;
+}
+
+/* Cuts [0, n_ref) into at most G ranges of about equal index size; returns
+ * the number of ranges, their starts in t0[] (t0[n] = n_ref). */
+static int cut_groups(const bai_t *a, const bai_t *b, int32_t n_ref, int G, int32_t *t0)
+{
+    double tot = 0;
+    for (int32_t t = 0; t < n_ref; ++t) tot += (double)a->ref[t].bytes + (double)b->ref[t].bytes;
+    int n = 0;
+    t0[n++] = 0;
+    double acc = 0;
+    for (int32_t t = 0; t < n_ref && n < G; ++t) {
+        acc += (double)a->ref[t].bytes + (double)b->ref[t].bytes;
+        if (acc >= tot * n / G && t + 1 < n_ref && acc > 0) t0[n++] = t + 1;
+    }
+    t0[n] = n_ref;
+    return n;
+}
+
+/* The contig-parallel run; returns 0 when it ran, 1 when the inputs do not
+ * allow it (no index, stdin, a single range), -1 on failure. */
+static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq, int bthreads, int cap,
+                      const char *fn_fa)
+{
+    int G = env_int("SS_CONTIG_GROUPS", 4);
+    if (G > 64) G = 64;
+    if (G < 2 || env_int("SS_PILEUP_THREADS", 2) != 2 || !strcmp(bam1, "-") || !strcmp(bam2, "-")) return 1;
+    bai_t *x1 = bai_load_for(bam1), *x2 = x1 ? bai_load_for(bam2) : NULL;
+    const int32_t n_ref = base->h1->n_ref;
+    if (!x1 || !x2 || x1->n_ref != n_ref || x2->n_ref < n_ref) { bai_free(x1); bai_free(x2); return 1; }
+    int32_t t0[65];
+    const int n = cut_groups(x1, x2, n_ref, G, t0);
+    if (n < 2) { bai_free(x1); bai_free(x2); return 1; }
+    group_t *g = (group_t *)calloc((size_t)n, sizeof(group_t));
+    int bad = 0;
+    for (int i = 0; i < n && !bad; ++i) {
+        group_t *q = &g[i];
+        q->bam1 = bam1;
+        q->bam2 = bam2;
+        q->t0 = t0[i];
+        q->t1 = t0[i + 1];
+        q->mapq = mapq;
+        q->bthreads = bthreads;
+        q->v1 = bai_first_at_or_after(x1, q->t0);
+        q->v2 = bai_first_at_or_after(x2, q->t0);
+        const col_seed_t none = {0, 0, 0, i + 1 < n ? q->t1 : INT32_MAX};
+        q->s1 = q->s2 = none;
+        int32_t tid;
+        int64_t pos;
+        const uint32_t mask = SS_BAM_DEF_MASK;
+        int r = bai_last_loaded_before(bam1, x1, q->t0, mask, mapq, &tid, &pos);
+        if (r < 0) bad = 1;
+        else if (r) { q->s1.has_prev = 1; q->s1.prev_tid = tid; q->s1.prev_pos = pos; }
+        r = bai_last_loaded_before(bam2, x2, q->t0, mask, mapq, &tid, &pos);
+        if (r < 0) bad = 1;
+        else if (r) { q->s2.has_prev = 1; q->s2.prev_tid = tid; q->s2.prev_pos = pos; }
+        if (timing)
+            fprintf(stderr, "[timing] group %d contigs [%d, %d) start %llx / %llx seed %d:%d:%lld / %d:%d:%lld\n", i,
+                    q->t0, q->t1, (unsigned long long)q->v1, (unsigned long long)q->v2, q->s1.has_prev, q->s1.prev_tid,
+                    (long long)q->s1.prev_pos, q->s2.has_prev, q->s2.prev_tid, (long long)q->s2.prev_pos);
+        run_t *R = &q->R;                                  /* the group's own run: fai handle, batches, scorers */
+        R->h1 = base->h1;
+        R->cur_tid = -1;
+        R->fai = fasta_index_load(fn_fa);
+        R->fmt = base->fmt;
+        R->out = open_memstream(&q->obuf, &q->olen);
+        if (base->dump) R->dump = open_memstream(&q->dbuf, &q->dlen);
+        R->pileup_only = base->pileup_only;
+        R->prm = base->prm;
+        R->n_dev = base->n_dev;
+        memcpy(R->device, base->device, sizeof R->device);
+        R->n_bat = R->n_dev + 3;
+        for (int k = 0; k < R->n_bat; ++k) batch_init(&R->bat[k], (size_t)cap);
+        pthread_mutex_init(&R->mu, NULL);
+        pthread_cond_init(&R->cv, NULL);
+    }
+    bai_free(x1);
+    bai_free(x2);
+    if (bad) {
+        fprintf(stderr, "[bam-somaticsniper] cannot read the indexed BAMs\n");
+        return -1;
+    }
+    pthread_t *th = (pthread_t *)calloc((size_t)n, sizeof(pthread_t));
+    for (int i = 0; i < n; ++i) pthread_create(&th[i], NULL, group_main, &g[i]);
+    int rc = 0;
+    for (int i = 0; i < n; ++i) {
+        pthread_join(th[i], NULL);
+        run_t *R = &g[i].R;
+        fclose(R->out);
+        if (R->dump) fclose(R->dump);
+        if (g[i].err || failed_get(R)) rc = -1;
+        fwrite(g[i].obuf, 1, g[i].olen, base->out);      /* contig order */
+        if (base->dump && g[i].dlen) fwrite(g[i].dbuf, 1, g[i].dlen, base->dump);
+        free(g[i].obuf);
+        free(g[i].dbuf);
+        for (int k = 0; k < R->n_bat; ++k) batch_free(&R->bat[k]);
+        for (int k = 0; k < R->n_dev; ++k)
+            if (R->ctx[k]) ss_ctx_destroy(R->ctx[k]);
+        fasta_index_free(R->fai);
+        free(R->cur_ref);
+        pthread_mutex_destroy(&R->mu);
+        pthread_cond_destroy(&R->cv);
+    }
+    free(th);
+    free(g);
+    stamp("contig groups done");
+    return rc;
+}
+
 int main(int argc, char *argv[])
 {
     t_start = now_s();
@@ -471,27 +643,24 @@ int main(int argc, char *argv[])
         if (devs && *devs && parse_devices(devs, R.device, &R.n_dev)) return 1;
         if (R.n_dev == 0) R.device[R.n_dev++] = env_int("SS_DEVICE", 0);
     }
-    R.n_bat = R.n_dev + 3;
-    for (int k = 0; k < R.n_bat; ++k) batch_init(&R.bat[k], (size_t)(cap > 0 ? cap : 1 << 20));
-    pthread_mutex_init(&R.mu, NULL);
-    pthread_cond_init(&R.cv, NULL);
     R.pileup_only = pileup_only;
     R.prm = prm;
-    scorer_arg_t sarg[MAX_DEV];
-    for (int k = 0; k < R.n_dev; ++k) {                 /* each creates its GPU scorer first */
-        sarg[k].R = &R;
-        sarg[k].k = k;
-        pthread_create(&R.th[k], NULL, scorer_main, &sarg[k]);
-    }
     ss_write_header(R.out, fmt, fn_fa, normal_id, tumor_id);
-    dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, env_int("SS_PILEUP_THREADS", 2), on_site, &R);
-    stamp("pileup done");
-    if (filling(&R)->n) submit(&R);
-    pthread_mutex_lock(&R.mu);
-    R.quit = 1;
-    pthread_cond_broadcast(&R.cv);
-    pthread_mutex_unlock(&R.mu);
-    for (int k = 0; k < R.n_dev; ++k) pthread_join(R.th[k], NULL);
+    const int bcap = cap > 0 ? cap : 1 << 20;
+    /* indexed inputs: contig groups in parallel (returns 1 when not applicable) */
+    const int grc = run_groups(&R, argv[optind], argv[optind + 1], mapq, bthreads, bcap, fn_fa);
+    if (grc < 0) failed_set(&R);
+    R.n_bat = grc == 1 ? R.n_dev + 3 : 0;
+    for (int k = 0; k < R.n_bat; ++k) batch_init(&R.bat[k], (size_t)bcap);
+    pthread_mutex_init(&R.mu, NULL);
+    pthread_cond_init(&R.cv, NULL);
+    if (grc == 1) {                                     /* the single streaming walk */
+        scorer_arg_t sarg[MAX_DEV];
+        run_scorers_start(&R, sarg);                    /* each creates its GPU scorer first */
+        dual_pileup_run(fp1, fp2, (int)SS_BAM_DEF_MASK, mapq, env_int("SS_PILEUP_THREADS", 2), on_site, &R);
+        stamp("pileup done");
+        run_scorers_finish(&R);
+    }
     bgzf_close(fp1);
     bgzf_close(fp2);
     bam_header_free(&h1);

@@ -53,6 +53,37 @@ def test_cli_pileup_under_sanitizers(san_build, datasets, kind):
             assert got == ref, (d, kind, mode)
 
 
+@pytest.mark.skipif(not os.path.exists(REF_DUMP), reason="reference dump CLI not built")
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_contig_groups_under_sanitizers(san_build, datasets, tmp_path, kind):
+    """The contig-parallel pileup (indexed copies of the datasets, 3 ranges:
+    per range two seeked BGZF readers with inflate pools, two column streams
+    and the merge, the ranges' memory streams concatenated at the end) under
+    ASan/UBSan and TSan; site streams equal the reference's."""
+    import shutil
+    index = os.path.join(ROOT, "somatic-sniper_amd", "ss-index")
+    if not os.path.exists(index):
+        pytest.skip("ss-index not built")
+    cli = os.path.join(san_build, f"bam-somaticsniper-{kind}")
+    for i, (d, fa, t, n) in enumerate(datasets):
+        dst = tmp_path / f"s{i}"
+        dst.mkdir()
+        for f in os.listdir(d):
+            if f.endswith((".bam", ".fa", ".fai")):
+                shutil.copy(os.path.join(d, f), dst / f)
+        if any(subprocess.run([index, b], cwd=str(dst), capture_output=True).returncode for b in (t, n)):
+            continue                          # the unsorted pair: no index, streaming walk
+        p = _run([REF_DUMP, "-f", fa, t, n, "ref_g.out"], str(dst), {"SS_DUMP_PILEUP": "ref_g.dump"})
+        assert p.returncode == 0, p.stderr
+        ref = (dst / "ref_g.dump").read_bytes() if (dst / "ref_g.dump").exists() else b""
+        p = _run([cli, "-f", fa, t, n, "g.out"], str(dst),
+                 {"SS_PILEUP_ONLY": "1", "SS_CONTIG_GROUPS": "3", "SS_DUMP_PILEUP": "g.dump"})
+        assert p.returncode == 0 and "Sanitizer" not in p.stderr and "runtime error" not in p.stderr, \
+            (d, p.stderr[-3000:])
+        got = (dst / "g.dump").read_bytes() if (dst / "g.dump").exists() else b""
+        assert got == ref, (d, kind)
+
+
 @pytest.mark.parametrize("kind", ["asan", "tsan"])
 def test_table_builder_under_sanitizers(san_build, tmp_path, kind):
     """Four threads building two parameter sets at once (8 coef threads each),
