@@ -172,6 +172,7 @@ static void put_ref(FILE *o, ref_acc_t *A)
         if (!A->lin[i]) A->lin[i] = A->lin[i - 1];
     fwrite(&A->n_lin, 4, 1, o);
     fwrite(A->lin, 8, (size_t)A->n_lin, o);
+    if (A->n_lin) memset(A->lin, 0, 8 * (size_t)A->n_lin);   /* the next contig starts empty */
     A->n_lin = 0;
 }
 

@@ -452,6 +452,11 @@ static void *group_main(void *arg)
         if (f2) bgzf_close(f2);
     }
     run_scorers_finish(R);
+    /* release the range's GPU contexts and batches here, while other ranges still run */
+    for (int k = 0; k < R->n_dev; ++k)
+        if (R->ctx[k]) { ss_ctx_destroy(R->ctx[k]); R->ctx[k] = NULL; }
+    for (int k = 0; k < R->n_bat; ++k) batch_free(&R->bat[k]);
+    R->n_bat = 0;
     return NULL;
 }
 
@@ -535,6 +540,7 @@ static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq,
         fprintf(stderr, "[bam-somaticsniper] cannot read the indexed BAMs\n");
         return -1;
     }
+    stamp("contig groups planned");
     pthread_t *th = (pthread_t *)calloc((size_t)n, sizeof(pthread_t));
     for (int i = 0; i < n; ++i) pthread_create(&th[i], NULL, group_main, &g[i]);
     int rc = 0;
@@ -548,9 +554,6 @@ static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq,
         if (base->dump && g[i].dlen) fwrite(g[i].dbuf, 1, g[i].dlen, base->dump);
         free(g[i].obuf);
         free(g[i].dbuf);
-        for (int k = 0; k < R->n_bat; ++k) batch_free(&R->bat[k]);
-        for (int k = 0; k < R->n_dev; ++k)
-            if (R->ctx[k]) ss_ctx_destroy(R->ctx[k]);
         fasta_index_free(R->fai);
         free(R->cur_ref);
         pthread_mutex_destroy(&R->mu);

@@ -22,6 +22,7 @@ CODE = {"A": 1, "C": 2, "G": 4, "T": 8}
 def make_bam(path, contigs, refs, depth, rng, seed_tag, read_len=100, vaf_tab=None):
     recs = []
     for ci, (name, seq) in enumerate(contigs):
+        print(f"[bamsim] {os.path.basename(path)}: contig {ci + 1}/{len(contigs)}", file=sys.stderr, flush=True)
         L = len(seq)
         n = int(L * depth / read_len)
         pos = np.sort(rng.integers(0, max(1, L - read_len), n)).astype(np.int32)

@@ -9,16 +9,24 @@ LEN=${1:-50000000}; DT=${2:-30}; DN=${3:-30}; NC=${4:-8}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 W=/tmp/ss_e2eg_$$
 mkdir -p "$W" "$R/gpurun_out"
-trap 'rm -rf "$W"' EXIT
+TICK=
+trap '[ -n "$TICK" ] && kill $TICK 2>/dev/null; rm -rf "$W"; true' EXIT
 ts() { date +%s.%N; }
+P=$R/gpurun_out/e2e_progress.log
+: > "$P"
+# progress for long silent steps: the step's name and elapsed seconds every 30 s
+tick() { local what=$1; local s=0; while sleep 30; do s=$((s + 30)); echo "$what ${s}s" >> "$P"; done; }
 t0=$(ts)
-timeout -k 10 900 python3 "$R/tools/bamsim.py" "$W" --length "$LEN" --depth-t "$DT" --depth-n "$DN" --contigs "$NC" >/dev/null
+timeout -k 10 900 python3 "$R/tools/bamsim.py" "$W" --length "$LEN" --depth-t "$DT" --depth-n "$DN" --contigs "$NC" >/dev/null 2>> "$P"
 t1=$(ts)
 cd "$W"
 timeout -k 10 300 "$R/somatic-sniper_amd/ss-index" tumor.bam
 timeout -k 10 300 "$R/somatic-sniper_amd/ss-index" normal.bam
 t2=$(ts)
+tick "reference CLI" & TICK=$!
 timeout -k 10 900 "$R/oracle/_ref/bam-somaticsniper" -f ref.fa tumor.bam normal.bam ref.out 2> ref.err
+kill $TICK; TICK=
+echo "reference done" >> "$P"
 t3=$(ts)
 SS_CONTIG_GROUPS=1 timeout -k 10 600 "$R/somatic-sniper_amd/bam-somaticsniper" -f ref.fa tumor.bam normal.bam s.out 2> s.err
 t4=$(ts)
