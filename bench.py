@@ -617,7 +617,7 @@ def main():
         "ranks": ranks,
         "roofline": {
             "bound": "hbm",
-            "kernel": {"main": "ss_score_main", "wide": "ss_score_wide", "deep": "ss_score_deep"}[dom],
+            "kernel": {"main": "ss_score_main", "wide": "ss_score_group", "deep": "ss_score_deep"}[dom],
             "achieved": round(achieved, 2) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

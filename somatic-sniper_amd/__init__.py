@@ -400,7 +400,7 @@ class Context:
 
     def kernel_time_log(self, kernel: str = "main") -> np.ndarray:
         """Durations (ms) of one kernel of every launch since set_kernel_timing(True):
-        "main" (ss_score_main), "wide" (ss_score_wide), "deep" (ss_score_deep) or "all" (the launch)."""
+        "main" (ss_score_main), "wide" (ss_score_group: the wide list), "deep" (ss_score_deep) or "all" (the launch)."""
         buf = np.zeros(4096, np.float64)
         n = self.lib.ss_kernel_time_log_k(self.h, self.KERNELS[kernel], buf.ctypes.data, buf.size)
         if n < 0:

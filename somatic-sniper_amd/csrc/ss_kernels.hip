@@ -1285,6 +1285,36 @@ __device__ __forceinline__ void ln_records(const uint32_t (&v)[LN_R], uint32_t n
  * are (x + 0.0 == x), so lanes of shorter chains need no mask. */
 #define LN_FK_ZERO 256
 
+/* four steps of a chain from the window R of records k0 - 3 .. k0; steps
+ * j >= m (past the chain's end) read fk's zero entry */
+template <bool TAIL>
+__device__ __forceinline__ void ln_steps(const char *fkb, uint32_t R, uint32_t m, uint32_t &W, float &e, float &f)
+{
+    double t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t r = R >> (24 - 8 * j);                     /* record k0 - j in the low byte */
+        const uint32_t sh = (r >> 2) & 16u;                       /* strand << 4 */
+        uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
+        if (TAIL) w8 = (uint32_t)j < m ? w8 : 8u * LN_FK_ZERO;
+        W += 8u << sh;
+        t[j] = *reinterpret_cast<const double *>(fkb + w8);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t q = (R >> (24 - 8 * j)) & 63u;
+        e = (float)((double)e + t[j] * (double)q);
+        f = (float)((double)f + t[j]);
+    }
+}
+
+/* window of records k0 - 3 .. k0 (k0 = s0 + n - 1 - i) at column byte k0 + 1 */
+__device__ __forceinline__ uint32_t ln_window(const uint32_t *colw, uint32_t b)
+{
+    const uint32_t row = (b >> 2) * 64u;
+    return __builtin_amdgcn_alignbyte(colw[row + 64u], colw[row], b & 3u);
+}
+
 __device__ __forceinline__ void ln_chain(const LaneLds &L, uint32_t lane, uint32_t s0, uint32_t n,
                                          const double *fk, float &e, float &f)
 {
@@ -1293,27 +1323,14 @@ __device__ __forceinline__ void ln_chain(const LaneLds &L, uint32_t lane, uint32
     e = 0.0f;
     f = 0.0f;
     uint32_t W = 0;                  /* strand 0 count in bits 0..15, strand 1 in 16..31 (units of 8 B) */
-    for (uint32_t i = 0; __ballot(i < n); i += 4u) {
-        /* window of records k0 - 3 .. k0 (k0 = s0 + n - 1 - i) at column byte k0 + 1 */
-        const uint32_t b = i < n ? s0 + n - i : 4u;
-        const uint32_t row = (b >> 2) * 64u;
-        const uint32_t R = __builtin_amdgcn_alignbyte(colw[row + 64u], colw[row], b & 3u);
-        double t[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t r = R >> (24 - 8 * j);                 /* record k0 - j in the low byte */
-            const uint32_t sh = (r >> 2) & 16u;                   /* strand << 4 */
-            const uint32_t w8 = i + (uint32_t)j < n ? __builtin_amdgcn_ubfe(W, sh, 16u) : 8u * LN_FK_ZERO;
-            W += 8u << sh;
-            t[j] = *reinterpret_cast<const double *>(fkb + w8);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t q = (R >> (24 - 8 * j)) & 63u;
-            e = (float)((double)e + t[j] * (double)q);
-            f = (float)((double)f + t[j]);
-        }
-    }
+    /* whole groups of four steps; a lane whose chain has fewer left sits
+     * them out (exec mask), so these steps need no end test */
+    for (uint32_t i = 0; __ballot(i + 4u <= n); i += 4u)
+        if (i + 4u <= n) ln_steps<false>(fkb, ln_window(colw, s0 + n - i), 4u, W, e, f);
+    /* the lane's last 1..3 steps */
+    const uint32_t i = n & ~3u;
+    if (__ballot(i < n))
+        if (i < n) ln_steps<true>(fkb, ln_window(colw, s0 + n - i), n - i, W, e, f);
 }
 
 /* fold of one sample: group sizes cnt (8-bit fields), records from s0 */
@@ -1909,6 +1926,288 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
 }
 
 /* --------------------------------------------------------------------------
+ * Group kernel: the wide list's sites with at most SS_WIDE_MAXSLOTS reads per
+ * sample, sorted by lane groups (round 3; replaces the wave-per-site network
+ * of ss_score_wide on the launch path).
+ *
+ * A sort unit is one (site, sample) of n reads; it takes U = 1, 2, 4, 8 or 16
+ * lanes (128 reads each).  Every lane builds and sorts its 128 keys exactly as
+ * the main kernel does (ln_keys, ln_levels: complemented high halves, packed
+ * min / max), then the unit's lanes merge across lanes, level 256 .. 128 U of
+ * the same flip-form bitonic network: a mirror stage with the partner lane
+ * lane ^ (M - 1), cleaners with lane ^ M/4 .. lane ^ 1 (DPP within a row of
+ * 16 lanes), the in-lane stage at distance 64 and the in-lane cleaners.  In a
+ * cross-lane stage the lower lane keeps the minimum elements: in this layout
+ * that is min in the low half and max in the (complemented) high half, one
+ * v_bfi_b32 per register with a per-lane mask.  Units are laid out by
+ * descending U, so every unit sits in one wave-sized batch of lanes and its
+ * lanes are aligned; a batch merges up to its largest U (lanes of smaller
+ * units sit the larger levels out).  The sorted contributing keys leave as
+ * the wide kernel's 8-bit fold records in the wave's arena, per unit in
+ * ascending order, and the 16-site fold, likelihoods and decision are the wide
+ * kernel's (finish_sub).
+ * ------------------------------------------------------------------------ */
+namespace {
+
+#define GP_ARENA 16384                     /* record bytes per wave (16 sites of ~1000 reads) */
+#define GP_UNITS (2 * GB)
+
+struct alignas(16) GroupLds {
+    uint8_t  arena[WIDE_WAVES][GP_ARENA];
+    Slot3    slot[WIDE_WAVES][2 * GB];
+    SlotRes  res[WIDE_WAVES][2 * GB];
+    uint32_t site[WIDE_WAVES][GB];
+    uint32_t refc[WIDE_WAVES][GB];
+    uint32_t ucnt[WIDE_WAVES][GP_UNITS][4];          /* per unit: counts of bases 0, 2 | 1, 3 (16-bit), rms, wild */
+    uint8_t  unit_of[WIDE_WAVES][GP_UNITS * 16];     /* lane position -> unit */
+};
+
+/* cross-lane compare-exchange: the lower lane keeps (min lo, max hi) */
+template <int LJ, bool MIRROR>
+__device__ __forceinline__ void gp_xstage(uint32_t (&v)[LN_R], uint32_t msk)
+{
+#pragma unroll
+    for (int r = 0; r < LN_R; ++r) {
+        const uint32_t o = xor_lane<LJ>(v[r]);
+        uint32_t mn, mx;
+        if (MIRROR) {                        /* partner element 127 - r: swap and complement */
+            const uint32_t c = ~o;
+            mn = pk_min_swo(v[r], c);
+            mx = pk_max_swo(v[r], c);
+        } else {
+            mn = pk_min(v[r], o);
+            mx = pk_max(v[r], o);
+        }
+        v[r] = (mn & msk) | (mx & ~msk);
+    }
+}
+
+/* in-lane stage at distance 64: element r (low half of r) against r + 64 (high half of 63 - r) */
+__device__ __forceinline__ void gp_stage64(uint32_t (&v)[LN_R])
+{
+#pragma unroll
+    for (int r = 0; r < LN_R / 2; ++r) {
+        const uint32_t x = v[r], y = v[LN_R - 1 - r];
+        v[r] = pk_min_swo(x, ~y);
+        v[LN_R - 1 - r] = pk_min_swo(y, ~x);
+    }
+}
+
+/* level 128 M of a unit (M lanes merged), lane index j inside the unit */
+template <int M>
+__device__ __forceinline__ void gp_level(uint32_t (&v)[LN_R], uint32_t j)
+{
+    gp_xstage<M - 1, true>(v, (j & (uint32_t)(M / 2)) ? 0xffff0000u : 0x0000ffffu);
+    if constexpr (M >= 16) gp_xstage<4, false>(v, (j & 4u) ? 0xffff0000u : 0x0000ffffu);
+    if constexpr (M >= 8) gp_xstage<2, false>(v, (j & 2u) ? 0xffff0000u : 0x0000ffffu);
+    if constexpr (M >= 4) gp_xstage<1, false>(v, (j & 1u) ? 0xffff0000u : 0x0000ffffu);
+    gp_stage64(v);
+    ln_clean<LN_R, 32>(v);
+}
+
+__device__ __forceinline__ uint32_t gp_lanes(uint32_t n)
+{
+    return n <= 128u ? 1u : n <= 256u ? 2u : n <= 512u ? 4u : n <= 1024u ? 8u : 16u;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
+{
+    __shared__ double fk[256];
+    __shared__ uint2 lut[LN_LUT_BYTES / 8];
+    __shared__ GroupLds L;
+    const unsigned long long acc0 = *a.deep_acc;
+    const uint32_t nsegs = min((uint32_t)(acc0 >> 32), a.deep_nseg), total = (uint32_t)acc0;
+    if (nsegs == 0u) return;
+    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
+    ln_lut_build(lut);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint8_t *arena = L.arena[wv];
+    Slot3 *slot = L.slot[wv];
+    SlotRes *res = L.res[wv];
+    uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
+    uint32_t (*ucnt)[4] = L.ucnt[wv];
+    uint8_t *unit_of = L.unit_of[wv];
+    const uint32_t cap = (uint32_t)a.m.cap_mapQ;
+    const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
+    for (;;) {
+        uint32_t ch = 0;
+        if (lane == 0u) ch = atomicAdd(a.wide_next, 1u);
+        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * GB;
+        if (first >= total) break;
+        const uint32_t nlist = total - first < GB ? total - first : GB;
+        /* the chunk's sites, lane k = entry k (as in ss_score_wide) */
+        const ss_score_args &k = kernarg_args();
+        uint32_t lo = 0, hi = nsegs;
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (k.deep_off[mid] <= first) lo = mid;
+            else hi = mid;
+        }
+        uint32_t c_s = 0, c_ot = 0, c_nt = 0, c_on = 0, c_nn = 0, c_ref = 0;
+        bool c_ok = false;
+        if (lane < nlist) {
+            const uint32_t p = first + lane;
+            uint32_t sg = lo;
+            while (sg + 1u < nsegs && k.deep_off[sg + 1u] <= p) ++sg;
+            c_s = k.deep_list[(size_t)k.deep_segs[sg] * k.deep_seg_cap + (p - k.deep_off[sg])];
+            c_ot = k.off_t[c_s];
+            const uint32_t ot1 = k.off_t[c_s + 1];
+            c_on = k.off_n[c_s];
+            const uint32_t on1 = k.off_n[c_s + 1];
+            const uint32_t rc = k.ref[c_s];
+            c_ref = rc | (uint32_t)ss_tab_nt16(k.m)[rc] << 8;
+            c_ok = c_ot <= ot1 && ot1 <= end_t && c_on <= on1 && on1 <= end_n &&
+                   ot1 - c_ot <= SS_WIDE_MAXSLOTS && on1 - c_on <= SS_WIDE_MAXSLOTS;
+            c_nt = c_ok ? ot1 - c_ot : 0u;
+            c_nn = c_ok ? on1 - c_on : 0u;
+            if (!c_ok) {                             /* malformed or too deep: the deep kernel */
+                const uint32_t d = atomicAdd(k.deep2_count, 1u);
+                if (d < k.deep_cap) k.deep2_list[d] = c_s;
+                else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
+            }
+        }
+        /* sub-groups of consecutive sites whose records fit the arena */
+        const uint32_t need = c_ok ? ((c_nt + 3u) & ~3u) + ((c_nn + 3u) & ~3u) : 0u;
+        uint32_t done = 0;
+        while (done < nlist) {
+            /* sites done .. done + G - 1 (inclusive prefix of `need` within the arena) */
+            uint32_t pre = lane >= done && lane < nlist ? need : 0u;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)pre, o);
+                if (lane >= (uint32_t)o) pre += t;
+            }
+            const uint64_t fit = __ballot(lane >= done && lane < nlist && pre <= GP_ARENA);
+            const uint32_t G = max(1u, (uint32_t)__popcll(fit));     /* a site always fits (2 x 2048 <= 16 K) */
+            const uint32_t s0 = done;
+            done += G;
+            /* units of the sub-group: lane u < 2G is unit u = (site s0 + u / 2, sample u & 1) */
+            const uint32_t us = s0 + (lane >> 1);
+            const bool is_u = lane < 2u * G;
+            const uint32_t s_nt = (uint32_t)__shfl((int)c_nt, (int)us), s_nn = (uint32_t)__shfl((int)c_nn, (int)us);
+            const uint32_t n_u = is_u ? ((lane & 1u) ? s_nn : s_nt) : 0u;
+            const uint32_t U_u = gp_lanes(n_u);
+            /* lane offsets by descending U (aligned, so a unit never straddles a batch) */
+            uint32_t off_u = 0, T = 0;
+#pragma unroll
+            for (uint32_t c = 16u; c >= 1u; c >>= 1) {
+                const uint64_t mk = __ballot(is_u && U_u == c);
+                if (is_u && U_u == c)
+                    off_u = T + c * __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                T += c * (uint32_t)__popcll(mk);
+            }
+            /* arena bases: units in order, records rounded up to 4 bytes */
+            uint32_t base = is_u ? ((n_u + 3u) & ~3u) : 0u;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)base, o);
+                if (lane >= (uint32_t)o) base += t;
+            }
+            base -= is_u ? ((n_u + 3u) & ~3u) : 0u;       /* exclusive */
+            if (is_u) {
+                for (uint32_t t = 0; t < U_u; ++t) unit_of[off_u + t] = (uint8_t)lane;
+                ucnt[lane][0] = ucnt[lane][1] = ucnt[lane][2] = ucnt[lane][3] = 0u;
+            }
+            wave_sync();
+            for (uint32_t b0 = 0; b0 < T; b0 += 64u) {
+                const uint32_t p = b0 + lane;
+                const bool act = p < T;
+                const uint32_t u = act ? unit_of[p] : 0u;
+                const uint32_t un = (uint32_t)__shfl((int)n_u, (int)u), uU = (uint32_t)__shfl((int)U_u, (int)u);
+                const uint32_t uoff = (uint32_t)__shfl((int)off_u, (int)u);
+                const uint32_t site_l = s0 + (u >> 1), smp = u & 1u;
+                const uint32_t r_ot = (uint32_t)__shfl((int)c_ot, (int)site_l), r_on = (uint32_t)__shfl((int)c_on, (int)site_l);
+                const uint32_t rofs = smp ? r_on : r_ot;
+                const uint32_t ref16 = (uint32_t)__shfl((int)c_ref, (int)site_l) >> 8;
+                const uint32_t j = p - uoff;
+                LaneIn in;
+                const int rem = act ? (int)un - (int)(128u * j) : 0;
+                in.na = (uint32_t)min(max(rem, 0), 128);
+                in.na4 = (in.na + 3u) & ~3u;
+                in.nb = 0u;
+                in.nca = in.na4 >> 2;
+                in.nab = in.na4;
+                const uint32_t *base_s = smp ? a.reads_n : a.reads_t;
+                const uint32_t start = act ? rofs + 128u * j : 0u;
+                in.pa = base_s + start;
+                in.pb = in.pa;
+                in.la = in.lb = 256u * (1u + smp * 16u + ref16);
+                const uint32_t nch = wave_max((in.nab + 3u) >> 2);
+                const uint32_t endv = smp ? end_n : end_t;
+                in.tail = __ballot((uint64_t)start + 4u * nch > (uint64_t)endv) || end_t < 4u || end_n < 4u;
+                uint32_t v[LN_R];
+                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
+                ln_levels<LN_R, 2>(v);
+                if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }
+                if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }
+                if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }
+                if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }
+                if (act) {
+                    const uint32_t c = acc.cnt_a;
+                    atomicAdd(&ucnt[u][0], c & 0x00ff00ffu);
+                    atomicAdd(&ucnt[u][1], (c >> 8) & 0x00ff00ffu);
+                    atomicAdd(&ucnt[u][2], acc.rms_a);
+                    if (acc.maxq >= 64u) ucnt[u][3] = 1u;     /* 8-bit records cannot hold its q */
+                }
+                wave_sync();
+                /* the unit's contributing keys as records, ascending */
+                const uint32_t ca = act ? ucnt[u][0] : 0u, cb = act ? ucnt[u][1] : 0u;
+                const uint32_t tot = (ca & 0xffffu) + (ca >> 16) + (cb & 0xffffu) + (cb >> 16);
+                const int lim = act ? min(max((int)tot - (int)(128u * j), 0), 128) : 0;
+                const uint32_t ubase = (uint32_t)__shfl((int)base, (int)u) + 128u * j;
+#pragma unroll
+                for (int i = 0; i < LN_C; ++i) {
+                    if (!__ballot(4 * i < lim)) break;
+                    if (4 * i < lim) {
+                        const uint32_t d = key_to_rec8(ln_elem(v, 4 * i)) | key_to_rec8(ln_elem(v, 4 * i + 1)) << 8 |
+                                           key_to_rec8(ln_elem(v, 4 * i + 2)) << 16 |
+                                           key_to_rec8(ln_elem(v, 4 * i + 3)) << 24;
+                        *reinterpret_cast<uint32_t *>(arena + ubase + 4u * (uint32_t)i) = d;
+                    }
+                }
+                wave_sync();
+            }
+            /* slots of the sites that stay (no wild read, well formed), compacted */
+            const uint32_t wild_u = is_u ? ucnt[lane][3] : 0u;
+            const uint64_t wildm = __ballot(wild_u != 0u);
+            const bool site_lane = lane >= s0 && lane < s0 + G;
+            const uint32_t su = lane - s0;                       /* this site lane's units 2su, 2su + 1 */
+            const bool stay = site_lane && c_ok && !((wildm >> (2u * su)) & 3u);
+            const uint64_t staym = __ballot(stay);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(staym >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)staym, 0u));
+            if (site_lane && c_ok && !stay) {                    /* a wild read: the deep kernel */
+                const uint32_t d = atomicAdd(k.deep2_count, 1u);
+                if (d < k.deep_cap) k.deep2_list[d] = c_s;
+                else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
+            }
+            /* unit lanes publish their slot under the site's rank */
+            const uint32_t rank_u = (uint32_t)__shfl((int)rank, (int)us);
+            const bool stay_u = is_u && ((staym >> us) & 1ull);
+            if (stay_u) {
+                Slot3 &st = slot[2u * rank_u + (lane & 1u)];
+                const uint32_t ca = ucnt[lane][0], cb = ucnt[lane][1];
+                st.rec_n = base | n_u << 16;
+                st.cnt01 = (ca & 0xffffu) | (cb & 0xffffu) << 16;
+                st.cnt23 = (ca >> 16) | (cb >> 16) << 16;
+                st.rms = ucnt[lane][2];
+            }
+            if (stay) {
+                sites[rank] = c_s;
+                refcs[rank] = c_ref;
+            }
+            const uint32_t G2 = (uint32_t)__popcll(staym);
+            wave_sync();
+            if (G2) finish_sub<uint8_t>(kernarg_args(), (int)G2, arena, slot, res, sites, refcs, fk);
+        }
+    }
+}
+
+/* --------------------------------------------------------------------------
  * Deep kernel: the sites the wide kernel cannot sort (more than
  * SS_WIDE_MAXSLOTS sort slots, any depth) and sites with malformed offsets.
  *
@@ -2216,7 +2515,11 @@ int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int de
     hipLaunchKernelGGL(ss_score_main, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[1], s);
+#ifndef SS_AB_OLDWIDE
+    hipLaunchKernelGGL(ss_score_group, dim3(wide_grid), dim3(SS_WIDE_BLOCK), 0, s, a);
+#else
     hipLaunchKernelGGL(ss_score_wide, dim3(wide_grid), dim3(SS_WIDE_BLOCK), 0, s, a);
+#endif
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[2], s);
     hipLaunchKernelGGL(ss_score_deep, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);

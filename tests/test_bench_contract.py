@@ -57,7 +57,7 @@ def test_bench_shard_workload_depth_baseline():
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["scaling"] == "weak" and r["config"]["sites_per_step_per_gpu"] == 65536
-    assert r["roofline"]["kernel"] == "ss_score_wide"
+    assert r["roofline"]["kernel"] == "ss_score_group"
     cb = r["cpu_baseline"]
     assert "500.0xT/500.0xN" in cb["sample"] and cb["parity_vs_gpu"] is True
 
