@@ -1097,12 +1097,6 @@ __device__ __forceinline__ uint32_t ln_elem(const uint32_t (&v)[R], int e)
     return e < R ? (v[e] & 0xffffu) : (~v[2 * R - 1 - e] >> 16);
 }
 
-/* 8-bit fold record of a key: clamped q (sniper_maqcns.c:165) | strand << 6 */
-__device__ __forceinline__ uint32_t ln_rec(uint32_t k)
-{
-    const uint32_t q = max((k >> 5) & 0xffu, (k & 1u) << 2);
-    return q | (k & 8u) << 3;
-}
 
 /* Key-build lookup table (LDS, per workgroup), 8-byte entries: for a read's
  * nt16 code and strand, the site's reference code and the sample, .x the
@@ -1265,15 +1259,47 @@ __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint2 *lut, u
     return acc;
 }
 
-/* sorted elements [0, nel) as records into the lane's LDS column */
-__device__ __forceinline__ void ln_records(const uint32_t (&v)[LN_R], uint32_t nel, LaneLds &L, uint32_t lane)
+/* The sorted registers become fold records in place, two per register:
+ * register r's elements r (low half) and 127 - r (high half, complemented)
+ * give records q | strand << 6 (| 1 << 7 with WIDE: the wide fold's fsum
+ * multiplier, key_to_rec8) in bytes 0 and 2, computed on both halves at once
+ * (q = max(minq, nz << 2), sniper_maqcns.c:165, for minq < 64 -- sites with a
+ * larger one are not scored from these records).  Registers whose elements
+ * are all past nel are left alone (wave-uniform bound). */
+template <bool WIDE>
+__device__ __forceinline__ void ln_to_records(uint32_t (&v)[LN_R], uint32_t nel)
 {
+#pragma unroll
+    for (int r = 0; r < LN_R; ++r) {
+        if ((uint32_t)r >= nel && (uint32_t)(LN_N - 1 - r) >= nel) continue;
+        const uint32_t x = v[r] ^ 0xffff0000u;                   /* both keys plain */
+        const uint32_t q = pk_max((x >> 5) & 0x003f003fu, (x << 2) & 0x00040004u);
+        v[r] = ((x << 3) & 0x00400040u) | q | (WIDE ? 0x00800080u : 0u);
+    }
+}
+
+/* records of elements 4i .. 4i + 3 from the converted registers, one dword */
+__device__ __forceinline__ uint32_t ln_rec_dword(const uint32_t (&v)[LN_R], int i)
+{
+    if (4 * i < LN_R) {              /* low halves of registers 4i .. 4i + 3 (byte 0 of each) */
+        const uint32_t a = __builtin_amdgcn_perm(v[4 * i + 1], v[4 * i], 0x0c0c0400u);
+        const uint32_t b = __builtin_amdgcn_perm(v[4 * i + 3], v[4 * i + 2], 0x04000c0cu);
+        return a | b;
+    }
+    const int r0 = LN_N - 1 - 4 * i;  /* high halves of registers r0, r0 - 1, r0 - 2, r0 - 3 (byte 2) */
+    const uint32_t a = __builtin_amdgcn_perm(v[r0 - 1], v[r0], 0x0c0c0602u);
+    const uint32_t b = __builtin_amdgcn_perm(v[r0 - 3], v[r0 - 2], 0x06020c0cu);
+    return a | b;
+}
+
+/* sorted elements [0, nel) as records into the lane's LDS column */
+__device__ __forceinline__ void ln_records(uint32_t (&v)[LN_R], uint32_t nel, LaneLds &L, uint32_t lane)
+{
+    ln_to_records<false>(v, nel);
 #pragma unroll
     for (int i = 0; i < LN_C; ++i) {
         if ((uint32_t)(4 * i) >= nel) continue;              /* wave-uniform */
-        const uint32_t d = ln_rec(ln_elem(v, 4 * i)) | ln_rec(ln_elem(v, 4 * i + 1)) << 8 |
-                           ln_rec(ln_elem(v, 4 * i + 2)) << 16 | ln_rec(ln_elem(v, 4 * i + 3)) << 24;
-        L.rec[i + 1][lane] = d;
+        L.rec[i + 1][lane] = ln_rec_dword(v, i);
     }
 }
 
@@ -2159,15 +2185,11 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
                 const uint32_t tot = (ca & 0xffffu) + (ca >> 16) + (cb & 0xffffu) + (cb >> 16);
                 const int lim = act ? min(max((int)tot - (int)(128u * j), 0), 128) : 0;
                 const uint32_t ubase = (uint32_t)__shfl((int)base, (int)u) + 128u * j;
+                ln_to_records<true>(v, wave_max((uint32_t)lim));
 #pragma unroll
                 for (int i = 0; i < LN_C; ++i) {
-                    if (!__ballot(4 * i < lim)) break;
-                    if (4 * i < lim) {
-                        const uint32_t d = key_to_rec8(ln_elem(v, 4 * i)) | key_to_rec8(ln_elem(v, 4 * i + 1)) << 8 |
-                                           key_to_rec8(ln_elem(v, 4 * i + 2)) << 16 |
-                                           key_to_rec8(ln_elem(v, 4 * i + 3)) << 24;
-                        *reinterpret_cast<uint32_t *>(arena + ubase + 4u * (uint32_t)i) = d;
-                    }
+                    if (!__ballot(4 * i < lim)) continue;
+                    if (4 * i < lim) *reinterpret_cast<uint32_t *>(arena + ubase + 4u * (uint32_t)i) = ln_rec_dword(v, i);
                 }
                 wave_sync();
             }
