@@ -104,6 +104,18 @@ def test_wide_sample_units_parity(pkg, oracle, lt, ln, fixed, n, wild, opts):
     assert_parity(pkg, oracle, batch, opts)
 
 
+@pytest.mark.parametrize("lt,ln,n", [(130, 126, 80), (255, 250, 60), (514, 508, 50), (1023, 1020, 30),
+                                     (2040, 40, 20), (140, 3, 60), (2, 600, 40)])
+@pytest.mark.parametrize("opts", [OPTSETS[0], OPTSETS[-1]])
+def test_group_unit_boundaries(pkg, oracle, lt, ln, n, opts):
+    """Lane-group sort units (ss_score_group) at every lane-count boundary:
+    Poisson depths straddling 128 / 256 / 512 / 1024 / 2048 reads per sample,
+    so units of 1, 2, 4, 8 and 16 lanes (and the deep kernel past 2048) mix in
+    one batch of lanes, plus sites with a tiny or empty second sample."""
+    batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, **EXOTIC), 11, n)
+    assert_parity(pkg, oracle, batch, opts)
+
+
 @pytest.mark.parametrize("opts", OPTSETS)
 def test_kernel_routing_mix(pkg, oracle, opts):
     """One batch whose sites take every route: main kernel (<= 512 sort slots),
