@@ -1349,10 +1349,19 @@ __device__ __forceinline__ void ln_chain(const LaneLds &L, uint32_t lane, uint32
     e = 0.0f;
     f = 0.0f;
     uint32_t W = 0;                  /* strand 0 count in bits 0..15, strand 1 in 16..31 (units of 8 B) */
-    /* whole groups of four steps; a lane whose chain has fewer left sits
-     * them out (exec mask), so these steps need no end test */
-    for (uint32_t i = 0; __ballot(i + 4u <= n); i += 4u)
-        if (i + 4u <= n) ln_steps<false>(fkb, ln_window(colw, s0 + n - i), 4u, W, e, f);
+    /* whole groups of four steps; a lane whose chain has fewer left computes
+     * them on a harmless window and keeps its old state (selects, not an exec
+     * mask: the masked form cost phi copies and exec bookkeeping every step,
+     * 4.5% of the kernel) */
+    for (uint32_t i = 0; __ballot(i + 4u <= n); i += 4u) {
+        const bool act = i + 4u <= n;
+        float e2 = e, f2 = f;
+        uint32_t W2 = W;
+        ln_steps<false>(fkb, ln_window(colw, act ? s0 + n - i : 3u), 4u, W2, e2, f2);
+        e = act ? e2 : e;
+        f = act ? f2 : f;
+        W = act ? W2 : W;
+    }
     /* the lane's last 1..3 steps */
     const uint32_t i = n & ~3u;
     if (__ballot(i < n))
