@@ -1025,6 +1025,7 @@ namespace {
 #define LN_WAVES (SS_MAIN_BLOCK / 64)
 
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 
 struct LaneLds {
     union {
@@ -1201,7 +1202,8 @@ __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint2 *lut, uin
         uint32_t vm;                                /* 0 or ~0 (the compiler's form: compare + select) */
         asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(vm) : "v"(valid), "i"(t));
         rd[t] = x[t] & vm;
-        minq[t] = min(rd[t] & 0xffu, (rd[t] >> 8) & 0xffu);
+        asm("v_min_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_1"
+            : "=v"(minq[t]) : "v"(rd[t]));                       /* min(mapQ, baseQ) in one op */
         lo6[t] = rd[t] & 0x3f00u;
         y[t] = rd[t] >> 13;
         /* contributing unless the clamped q is 0 (sniper_maqcns.c:165-167) */
@@ -1215,11 +1217,18 @@ __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint2 *lut, uin
         /* E = baseQ >> 6 at bit 1, nz = (baseQ & 0x3f) != 0 at bit 0 */
         const uint32_t key = ent[t].x | minq[t] << 5 | (y[t] & 6u) | ln_nz(lo6[t]);   /* < 2^16 */
         ccnt += ent[t].y;
-        const uint32_t tq = min(rd[t] & 0x7fu, cap);
-        crms += tq * tq;
         const uint32_t e = c4 + (uint32_t)t;
         if (e < LN_R) v[e] = key;                                   /* high half 0: a pad, see below */
         else v[LN_N - 1 - e] |= (key ^ 0xffffu) << 16;
+    }
+    /* rms terms min(mapQ & 0x7f, cap)^2 two at a time: the mapQ bytes of two
+     * reads in the halves of one register, clamped with v_pk_min_u16 and
+     * squared + summed by v_dot2_u32_u16 */
+#pragma unroll
+    for (int t = 0; t < 4; t += 2) {
+        uint32_t p = __builtin_amdgcn_perm(rd[t + 1], rd[t], 0x0c040c00u) & 0x007f007fu;
+        p = pk_min(p, cap * 0x10001u);
+        crms = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p), __builtin_bit_cast(u16x2_t, p), crms, false);
     }
     /* totals and A's share (B's = total - A's); crms < 2^24 */
     acc.rms_b += crms;
