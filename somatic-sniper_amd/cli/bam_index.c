@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 
 #include "bam_reader.h"
 #include "bgzf_reader.h"
@@ -58,19 +59,46 @@ bad:
     return NULL;
 }
 
+/* an index older than its BAM is stale (htslib's test, hts.c idx_test_and_fetch):
+ * it may describe a file since rewritten, so it is not used */
+static bai_t *bai_load_fresh(const char *idx_path, const struct stat *bam_st)
+{
+    struct stat st;
+    if (stat(idx_path, &st) != 0) return NULL;
+    if (st.st_mtim.tv_sec < bam_st->st_mtim.tv_sec ||
+        (st.st_mtim.tv_sec == bam_st->st_mtim.tv_sec && st.st_mtim.tv_nsec < bam_st->st_mtim.tv_nsec))
+        return NULL;
+    return bai_load(idx_path);
+}
+
 bai_t *bai_load_for(const char *bam_path)
 {
+    struct stat bst;
+    if (stat(bam_path, &bst) != 0) return NULL;
     const size_t n = strlen(bam_path);
     char *p = (char *)malloc(n + 5);
     snprintf(p, n + 5, "%s.bai", bam_path);
-    bai_t *x = bai_load(p);
+    bai_t *x = bai_load_fresh(p, &bst);
     if (!x && n > 4 && strcmp(bam_path + n - 4, ".bam") == 0) {
         memcpy(p, bam_path, n - 4);
         memcpy(p + n - 4, ".bai", 5);
-        x = bai_load(p);
+        x = bai_load_fresh(p, &bst);
     }
     free(p);
     return x;
+}
+
+int bai_check_start(const char *bam_path, uint64_t v, int32_t t0, int32_t n_ref)
+{
+    bgzf_reader_t *fp = bgzf_open_at(bam_path, 0, v);
+    if (!fp) return -1;
+    bam_record_t rec;
+    memset(&rec, 0, sizeof rec);
+    const int rc = bam_record_read(fp, &rec);
+    const int ok = rc > 0 && rec.tid >= t0 && rec.tid < n_ref && rec.pos >= -1;
+    bam_record_free(&rec);
+    bgzf_close(fp);
+    return ok ? 0 : -1;
 }
 
 void bai_free(bai_t *x)
@@ -212,6 +240,9 @@ int bai_build(const char *bam_path, const char *out_path)
         const int64_t beg = rec.pos < 0 ? 0 : rec.pos;
         int64_t end = (int64_t)bam_rec_end(&rec);
         if (end <= beg) end = beg + 1;
+        /* BAI bins and linear windows cover [0, 2^29) only (SAM spec 5.2; samtools
+         * index asks for CSI beyond): a longer contig cannot be indexed here */
+        if (end > ((int64_t)1 << 29)) { err = 1; break; }
         chunks_t *C = &A->bins[reg2bin(beg, end)];
         if (C->n && C->c[C->n - 1] == v0) C->c[C->n - 1] = v1;      /* contiguous: extend */
         else {

@@ -20,7 +20,8 @@ typedef struct {
     bai_ref_t *ref;
 } bai_t;
 
-/* path.bai, or path with ".bam" replaced by ".bai"; NULL if neither loads */
+/* path.bai, or path with ".bam" replaced by ".bai"; NULL if neither loads or
+ * the index is older than the BAM (stale) */
 bai_t *bai_load_for(const char *bam_path);
 void bai_free(bai_t *x);
 /* Writes the index of bam_path to out_path; 0 on success. */
@@ -35,5 +36,8 @@ int bai_last_loaded_before(const char *bam_path, const bai_t *x, int32_t t0, uin
                            int32_t *tid, int64_t *pos);
 /* Virtual offset of the first record of contig t0 or later (UINT64_MAX: none). */
 uint64_t bai_first_at_or_after(const bai_t *x, int32_t t0);
+/* 0 when the record at virtual offset v reads back and lies on a contig in
+ * [t0, n_ref): the index agrees with the file there; -1 otherwise. */
+int bai_check_start(const char *bam_path, uint64_t v, int32_t t0, int32_t n_ref);
 
 #endif

@@ -303,6 +303,12 @@ static int on_site(int32_t tid, int32_t pos, int n1, int n2, const uint32_t *pk1
                    const uint32_t *pk2, int np2, void *data)
 {
     run_t *R = (run_t *)data;
+    if (tid < 0 || tid >= R->h1->n_ref) {       /* a record naming no header contig */
+        fprintf(stderr, "[bam-somaticsniper] BAM record on contig %d: the header has %d\n", (int)tid,
+                (int)R->h1->n_ref);
+        failed_set(R);
+        return 1;
+    }
     if (R->fai && tid != R->cur_tid) {          /* contig cache (somatic_sniper.c:112-117) */
         free(R->cur_ref);
         R->cur_ref = fasta_fetch(R->fai, R->h1->name[tid], &R->cur_len);
@@ -492,7 +498,7 @@ static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq,
     const int n = cut_groups(x1, x2, n_ref, G, t0);
     if (n < 2) { bai_free(x1); bai_free(x2); return 1; }
     group_t *g = (group_t *)calloc((size_t)n, sizeof(group_t));
-    int bad = 0;
+    int bad = 0, stale = 0;
     for (int i = 0; i < n && !bad; ++i) {
         group_t *q = &g[i];
         q->bam1 = bam1;
@@ -503,6 +509,13 @@ static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq,
         q->bthreads = bthreads;
         q->v1 = bai_first_at_or_after(x1, q->t0);
         q->v2 = bai_first_at_or_after(x2, q->t0);
+        /* an index that does not agree with its file (stale, or another file's)
+         * would seek mid-record or to the wrong contig: the streaming walk runs */
+        if ((q->v1 != UINT64_MAX && bai_check_start(bam1, q->v1, q->t0, n_ref)) ||
+            (q->v2 != UINT64_MAX && bai_check_start(bam2, q->v2, q->t0, x2->n_ref))) {
+            stale = 1;
+            break;
+        }
         const col_seed_t none = {0, 0, 0, i + 1 < n ? q->t1 : INT32_MAX};
         q->s1 = q->s2 = none;
         int32_t tid;
@@ -536,6 +549,23 @@ static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq,
     }
     bai_free(x1);
     bai_free(x2);
+    if (stale) {                                          /* nothing started yet: plain walk */
+        if (timing) fprintf(stderr, "[timing] index does not match the BAM: streaming walk\n");
+        for (int i = 0; i < n; ++i) {
+            run_t *R = &g[i].R;
+            if (!R->out) continue;
+            fclose(R->out);
+            if (R->dump) fclose(R->dump);
+            free(g[i].obuf);
+            free(g[i].dbuf);
+            fasta_index_free(R->fai);
+            for (int k = 0; k < R->n_bat; ++k) batch_free(&R->bat[k]);
+            pthread_mutex_destroy(&R->mu);
+            pthread_cond_destroy(&R->cv);
+        }
+        free(g);
+        return 1;
+    }
     if (bad) {
         fprintf(stderr, "[bam-somaticsniper] cannot read the indexed BAMs\n");
         return -1;

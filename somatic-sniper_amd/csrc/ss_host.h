@@ -27,7 +27,7 @@ typedef struct ss_host_model {
     void    *shared;        /* the process-wide table entry coef / lhet belong to */
 } ss_host_model_t;
 
-extern unsigned char ss_nt16_table[256];   /* valid after ss_host_model_build */
+extern const unsigned char ss_nt16_table[256];   /* immutable (bam_import.c:23-40) */
 extern const int ss_genotype_nt16[10];
 
 int      ss_host_model_build(const ss_params_t *p, ss_host_model_t *m);

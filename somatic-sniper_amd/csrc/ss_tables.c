@@ -67,23 +67,30 @@ int ss_model_pinned(const uint64_t h[3])
     return 0;
 }
 
-unsigned char ss_nt16_table[256];
-
-static void nt16_table_init(void)
-{
-    /* samtools-0.1.6 bam_nt16_table (bam_import.c:23-40): IUPAC letters in both
-     * cases map to their 4-bit code, '=' to 0, colour digits 0-3 to A,C,G,T,
-     * everything else to 15 (N). */
-    static const char iupac[] = "=ACMGRSVTWYHKDBN";
-    int c;
-    for (c = 0; c < 256; ++c) ss_nt16_table[c] = 15;
-    for (c = 0; c < 16; ++c) {
-        unsigned char ch = (unsigned char)iupac[c];
-        ss_nt16_table[ch] = (unsigned char)c;
-        if (ch >= 'A' && ch <= 'Z') ss_nt16_table[ch | 0x20] = (unsigned char)c;
-    }
-    for (c = 0; c < 4; ++c) ss_nt16_table['0' + c] = (unsigned char)(1 << c);
-}
+/* samtools-0.1.6 bam_nt16_table (bam_import.c:23-40): the IUPAC letters of
+ * "=ACMGRSVTWYHKDBN" in both cases map to their 4-bit code, '=' to 0, colour
+ * digits 0-3 to A,C,G,T, everything else to 15 (N).  Immutable and initialised
+ * at load time: contexts created concurrently from several threads upload it
+ * while others are being built, so it must never be written at run time
+ * (tests/test_abi_cpu.py::test_nt16_table_immutable_under_concurrent_builds). */
+const unsigned char ss_nt16_table[256] = {
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+     1,  2,  4,  8, 15, 15, 15, 15, 15, 15, 15, 15, 15,  0, 15, 15,   /* '0'-'3', '=' */
+    15,  1, 14,  2, 13, 15, 15,  4, 11, 15, 15, 12, 15,  3, 15, 15,   /* '@' 'A'..'O' */
+    15, 15,  5,  6,  8, 15,  7,  9, 15, 10, 15, 15, 15, 15, 15, 15,   /* 'P'..'_'     */
+    15,  1, 14,  2, 13, 15, 15,  4, 11, 15, 15, 12, 15,  3, 15, 15,   /* '`' 'a'..'o' */
+    15, 15,  5,  6,  8, 15,  7,  9, 15, 10, 15, 15, 15, 15, 15, 15,   /* 'p'..DEL     */
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+    15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,
+};
 
 uint64_t ss_fnv1a64(const void *p, size_t n)
 {
@@ -493,7 +500,6 @@ int ss_host_model_build(const ss_params_t *p, ss_host_model_t *m)
     if (!p || p->n_hap < 2 || p->n_hap > 255 || !(p->theta > 0.0f) || p->cap_mapQ < 0)
         return SS_E_INVAL;
     pthread_mutex_lock(&g_tab_lock);
-    nt16_table_init();
     rc = tab_get(p, &t, &source);
     pthread_mutex_unlock(&g_tab_lock);
     if (rc != SS_OK) return rc;

@@ -12,7 +12,10 @@ host-side concatenation of per-rank outputs in (tid, pos) order.
   LPT start and from seeded random starts, keeping the plan with the smallest
   maximum load.  Deterministic for a given (lengths, world).  On GRCh38's 24
   primary contigs the largest rank holds 1.0040x the mean at 8 ranks (LPT
-  alone: 1.0363x), 1.00017x at 4 and 1.0000001x at 2.
+  alone: 1.0363x), 1.00017x at 4 and 1.0000001x at 2.  Assemblies with more than
+  ``LOCAL_SEARCH_MAX`` contigs (alts, decoys, scaffolds) get LPT alone: the
+  search's n x n move matrices would cost far more than they gain there, and
+  with thousands of small contigs LPT is already within one contig of the mean.
 * ``GRCH38_PRIMARY``  (name, length) of GRCh38 chr1..22, X, Y -- config C4's
   genome (BASELINE.json configs[3]).
 * ``shard_range``    contiguous equal split of a site range (synthetic shards).
@@ -45,16 +48,21 @@ def _lpt(lengths, world: int):
     return a
 
 
+LOCAL_SEARCH_MAX = 256
+
+
 def _descend(x, a, world: int):
     """Steepest descent on the sum of squared rank loads over single moves
     (contig t to rank r) and pairwise swaps (contigs t, u of different
-    ranks); returns the local optimum (assignment, loads)."""
+    ranks); returns the local optimum (assignment, loads).  At most 4 n
+    improving steps (each strictly lowers the objective, so it ends anyway;
+    the cap bounds the time)."""
     import numpy as np
     n = len(x)
     a = np.array(a, dtype=np.int64)
     loads = np.bincount(a, weights=x, minlength=world)
     idx = np.arange(n)
-    while True:
+    for _ in range(4 * n + 4):
         own = loads[a]
         dm = (own[:, None] - x[:, None]) ** 2 + (loads[None, :] + x[:, None]) ** 2 \
             - own[:, None] ** 2 - loads[None, :] ** 2
@@ -77,6 +85,7 @@ def _descend(x, a, world: int):
             loads[o] += x[u] - x[t]
             loads[r] += x[t] - x[u]
             a[t], a[u] = r, o
+    return a, loads
 
 
 def shard_contigs(lengths, world: int, restarts: int = 200, seed: int = 12345):
@@ -95,6 +104,11 @@ def shard_contigs(lengths, world: int, restarts: int = 200, seed: int = 12345):
         return [[] for _ in range(world)]
     x = np.asarray([float(v) for v in lengths], dtype=np.float64)
     x = x / max(x.max(), 1.0)
+    if len(x) > LOCAL_SEARCH_MAX:               # large assemblies: LPT only
+        plan = [[] for _ in range(world)]
+        for tid, r in enumerate(_lpt(lengths, world)):
+            plan[r].append(tid)
+        return [sorted(p) for p in plan]
     a, loads = _descend(x, _lpt(lengths, world), world)
     best = (float(loads.max()), a.copy())
     rng = np.random.default_rng(seed)

@@ -12,6 +12,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
 
 
+# Kernel-vs-oracle evidence first: under `pytest -x` a host-side (CLI) failure
+# still fails the run, but can no longer hide the HIP parity suite behind it.
+_FIRST = ["test_gpu_parity.py", "test_reference_unit.py", "test_multi_rank.py", "test_oracle_golden.py",
+          "test_abi_cpu.py", "test_bench_contract.py", "test_cli_shim.py", "test_cli_native.py"]
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        name = os.path.basename(str(item.fspath))
+        return _FIRST.index(name) if name in _FIRST else len(_FIRST)
+    items.sort(key=rank)                     # stable: order within a file is kept
+
+
 def pytest_sessionstart(session):
     # a fresh checkout: build the tree (library, CLI, oracle, and the reference
     # harness when /root/reference is here) before collection, since some

@@ -306,3 +306,114 @@ def test_multi_scorer_output_identical(datasets):
             ref = strip(open(os.path.join(d, "ref_ms.out")).read())
             assert strip(open(os.path.join(d, "one_ms.out")).read()) == ref
             assert strip(open(os.path.join(d, "three_ms.out")).read()) == ref, (d, fmt)
+
+
+def _grouped_dump(d, fa, t, n, groups="3", opts=()):
+    name = "chk.dump"
+    p = _run([NATIVE] + list(opts) + ["-f", fa, t, n, "out_chk"], str(d),
+             {"SS_DUMP_PILEUP": name, "SS_PILEUP_ONLY": "1", "SS_CONTIG_GROUPS": groups, "SS_TIMING": "1"})
+    assert p.returncode == 0, p.stderr
+    path = d / name
+    return (path.read_bytes() if path.exists() else b""), "contig groups done" in p.stderr
+
+
+@need_native
+@need_dump
+@need_index
+def test_stale_or_foreign_index_takes_streaming_walk(tmp_path):
+    """The reference never reads an index, so one that does not describe its
+    BAM must not change a byte: an index older than its BAM (htslib's
+    staleness test) and another file's index (records at the wrong offsets)
+    are both refused, the streaming walk runs, and the site stream equals the
+    reference's.  A fresh, matching index runs the contig groups."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bamgen
+    fa, t, n = "ref.fa", "tumor.bam", "normal.bam"
+    d, d5 = tmp_path / "src", tmp_path / "src5"
+    for x, seed, dep in ((d, 12, (4, 3)), (d5, 13, (5, 4))):
+        x.mkdir()
+        bamgen.make_pair(str(x), seed=seed, lengths=(20000,) * 8, depth_t=dep[0], depth_n=dep[1])
+    d, d5 = str(d), str(d5)
+    ref = _dump(REF_DUMP, d, fa, t, n, [], native=False)
+    dst = tmp_path / "fresh"
+    assert _indexed_copy(d, fa, t, n, dst)
+    got, grouped = _grouped_dump(dst, fa, t, n)
+    assert got == ref and grouped
+    # stale: the BAM rewritten (same bytes) after its index was made
+    st = os.stat(dst / t)
+    os.utime(dst / (t + ".bai"), ns=(st.st_atime_ns, st.st_mtime_ns - 10 ** 9))
+    got, grouped = _grouped_dump(dst, fa, t, n)
+    assert got == ref and not grouped
+    # foreign: the tumor BAM carries another dataset's index (same contig count)
+    dst2 = tmp_path / "foreign"
+    assert _indexed_copy(d, fa, t, n, dst2)
+    other = tmp_path / "other"
+    assert _indexed_copy(d5, fa, t, n, other)
+    shutil.copy(other / (t + ".bai"), dst2 / (t + ".bai"))
+    got, grouped = _grouped_dump(dst2, fa, t, n)
+    assert got == ref and not grouped
+
+
+def _htslib_layout(src, dst):
+    """Rewrite an ss-index BAI the way htslib's `samtools index` lays it out
+    (hts.c hts_idx_finish / update_loff): a pseudo-bin 37450 per placed contig
+    (its [first, last) offsets and mapped / unmapped counts), leading linear-index
+    windows before the first read set to the contig's first offset instead of 0,
+    and the trailing n_no_coor count."""
+    import struct
+    b = open(src, "rb").read()
+    o = 8
+    n_ref = struct.unpack_from("<i", b, 4)[0]
+    out = bytearray(b[:8])
+    for _ in range(n_ref):
+        n_bin = struct.unpack_from("<i", b, o)[0]
+        o += 4
+        bins, lo, hi = [], None, None
+        for _ in range(n_bin):
+            bin_id, n_chunk = struct.unpack_from("<Ii", b, o)
+            chunks = struct.unpack_from(f"<{2 * n_chunk}Q", b, o + 8)
+            bins.append(b[o:o + 8 + 16 * n_chunk])
+            o += 8 + 16 * n_chunk
+            lo = min([lo] + list(chunks[0::2])) if lo is not None else min(chunks[0::2])
+            hi = max([hi] + list(chunks[1::2])) if hi is not None else max(chunks[1::2])
+        n_intv = struct.unpack_from("<i", b, o)[0]
+        lin = list(struct.unpack_from(f"<{n_intv}Q", b, o + 4))
+        o += 4 + 8 * n_intv
+        if n_bin:
+            bins.append(struct.pack("<Ii4Q", 37450, 2, lo, hi, 1000, 3))
+            k = 0
+            while k < len(lin) and lin[k] == 0:
+                lin[k] = lo
+                k += 1
+        out += struct.pack("<i", len(bins)) + b"".join(bins)
+        out += struct.pack("<i", n_intv) + struct.pack(f"<{n_intv}Q", *lin)
+    assert o == len(b)
+    out += struct.pack("<Q", 7)                 # n_no_coor
+    open(dst, "wb").write(bytes(out))
+
+
+@need_native
+@need_dump
+@need_index
+@pytest.mark.parametrize("opts", [[], ["-q", "40"]])
+def test_contig_groups_with_htslib_layout_index(tmp_path, opts):
+    """Indexes as htslib writes them (pseudo-bin, filled leading linear-index
+    windows, n_no_coor) drive the contig groups to the reference's site stream
+    too, for 2..9 ranges over contigs spanning several linear windows."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bamgen
+    d = tmp_path / "hts"
+    d.mkdir()
+    bamgen.make_pair(str(d), seed=11, lengths=(70000, 400, 50000, 300, 30000), depth_t=6, depth_n=5,
+                     odd_cigars=True, unmapped=True)
+    for b in ("tumor.bam", "normal.bam"):
+        assert subprocess.run([INDEX, b, str(d / (b + ".ss.bai"))], cwd=str(d)).returncode == 0
+        _htslib_layout(d / (b + ".ss.bai"), d / (b + ".bai"))
+        assert (d / (b + ".bai")).read_bytes() != (d / (b + ".ss.bai")).read_bytes()
+    ref = _dump(REF_DUMP, str(d), "ref.fa", "tumor.bam", "normal.bam", opts, native=False)
+    assert ref
+    for groups in ("2", "3", "5", "9"):
+        got, grouped = _grouped_dump(d, "ref.fa", "tumor.bam", "normal.bam", groups, opts)
+        assert grouped and got == ref, (opts, groups)

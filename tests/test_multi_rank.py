@@ -83,6 +83,24 @@ def test_shard_contigs_partition():
     assert sh.shard_range(10, 3, 0) == (0, 4) and sh.shard_range(10, 3, 2) == (7, 10)
 
 
+def test_shard_contigs_large_assembly_is_fast():
+    """Thousands of contigs (GRCh38 with alts and decoys, scaffold assemblies):
+    LPT only, a partition within one contig of the mean, in well under a second."""
+    import importlib
+    import time
+    from __graft_entry__ import load_package
+    load_package()
+    sh = importlib.import_module("somatic_sniper_amd.sharding")
+    rng = np.random.default_rng(3)
+    lengths = [248956422, 242193529] + rng.integers(1000, 5_000_000, 4000).tolist()
+    t0 = time.perf_counter()
+    plan = sh.shard_contigs(lengths, 8)
+    assert time.perf_counter() - t0 < 2.0
+    assert sorted(t for p in plan for t in p) == list(range(len(lengths)))
+    loads = [sum(lengths[t] for t in p) for p in plan]
+    assert max(loads) <= sum(lengths) / 8 + max(lengths)
+
+
 # ------------------------------------------------------------------ GPU ranks
 def _gpu_worker(rank, world, port, out_dir):
     """One rank of a region-sharded run on the HIP path: its own context on
@@ -257,3 +275,48 @@ def test_contexts_do_not_wait_for_each_other(pkg):
     finally:
         ca.close()
         cb.close()
+
+
+@pytest.mark.gpu
+def test_concurrent_context_creation(pkg):
+    """8 threads create contexts on cuda:0 at the same moment (a barrier),
+    half with default tables and half with -T 0.9 (a table build in flight
+    while the others upload), three rounds; each context scores the same
+    60x/30x batch with many candidates and must equal the oracle on scores,
+    glf records and calls.  Round 3's CLI lost emitted records this way: a
+    context uploaded the nt16 table while another build rewrote it
+    (the reference emits every candidate,
+    sniper_pileup.c:256-258)."""
+    import threading
+    from oracle import binding as ob
+    b = pkg.synth_batch_host(pkg.Synth.default(60, 30, p_somatic=0.03, p_germline=0.02), 17, 6000)
+    want = {}
+    for th in (0.85, 0.9):
+        o = ob.Oracle(ob.opts_to_params([] if th == 0.85 else ["-T", "0.9"]))
+        want[th] = o.score_batch(b.ref, b.off_tumor, b.off_normal, b.reads_tumor, b.reads_normal)
+        assert len(want[th][1]) > 50
+    for rnd in range(3):
+        bar = threading.Barrier(8)
+        res, errs = [None] * 8, []
+
+        def work(i):
+            th = 0.85 if i % 2 == 0 else 0.9
+            try:
+                bar.wait()
+                with pkg.Context(pkg.Params.default(theta=th), device=0) as c:
+                    res[i] = (th, c.score_batch(b, want_glf=True))
+                    c.check()
+            except Exception as e:          # noqa: BLE001 -- reported below
+                errs.append(repr(e))
+
+        ts = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs, errs
+        for i, (th, (score, calls, glf)) in enumerate(res):
+            o_score, o_calls, o_glf = want[th]
+            assert (score == o_score).all(), (rnd, i, int((score != o_score).sum()))
+            assert (glf.view(np.uint8) == o_glf.view(np.uint8)).all(), (rnd, i)
+            assert len(calls) == len(o_calls) and (calls.view(np.uint8) == o_calls.view(np.uint8)).all(), (rnd, i)
