@@ -3,20 +3,23 @@
 
 Workload c4 (default; BASELINE.json configs[3]): the 24 GRCh38 primary contigs
 as a synthetic genome (one pileup site per position, 60xT/30xN Poisson depths,
-SURVEY.md 8(d)), divided by --c4-scale (16: 1.93e8 sites, which fits one
-GPU's HBM at N=1), contigs assigned to ranks by sharding.shard_contigs.  Sites
+SURVEY.md 8(d)), contigs assigned to ranks by sharding.shard_contigs.  Sites
 are keyed by (contig, position): synth shard = contig index.  One STEP = every
-rank scores its share of the genome once (ss_score_batch_device per contig:
-main + wide + deep kernels) -- total work fixed, strong scaling.  Workload
-shard: --sites sites per rank per step (weak scaling; the C2/C3/C5 depth
-runs).  Inputs are generated on the device before timing; the timed region
-contains only scoring.
+rank scores its share of the genome once (ss_score_batch_device per launch of
+up to --chunk sites: main + group + deep kernels).  By default the genome is
+divided by 8 / N (--c4-scale auto): every GPU holds one eighth of GRCh38
+(3.86e8 sites, about 143 GB of packed reads in HBM), so N = 8 scores the whole
+3.09e9-site genome of configs[3] in one step and N = 1, 2, 4 the same
+per-GPU share (weak scaling: per-GPU work fixed).  A secondary line,
+"strong_scaling", times the genome / 16 at every N (total work fixed).
+Workload shard: --sites sites per rank per step (weak scaling; the C2/C3/C5
+depth runs).  Inputs are generated on the device before timing; the timed
+region contains only scoring.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL backend only for the
 barrier and the max-over-ranks timing reduction).  Each rank scores its own
 contigs -- no collective on the data path.  value = sites scored by all ranks
-/ max rank time.  A secondary weak-scaling line (an equal synthetic shard per
-GPU) is reported as "weak_scaling".  Launched either
+/ max rank time.  Launched either
 by torch.distributed.run (RANK/WORLD_SIZE/LOCAL_RANK in the environment) or
 directly as ``bench.py --gpus N``: the parent then starts N fresh rank
 processes itself before anything touches the GPU, stays GPU-free, and relays
@@ -187,9 +190,9 @@ PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
 
 
 def pmc_child(args):
-    """--pmc-child: the bench's own launches (rank 0 of a 1-GPU run: every c4
-    contig, or the shard workload's batch 0), scored --pmc-launches passes,
-    nothing else (run under rocprofv3 by live_counters)."""
+    """--pmc-child: the bench's own launches (rank 0 of a 1-GPU run: the first
+    --pmc-batches c4 launches, or the shard workload's batch 0), scored
+    --pmc-launches passes, nothing else (run under rocprofv3 by live_counters)."""
     import torch
     from __graft_entry__ import load_package
     pkg = load_package()
@@ -197,7 +200,7 @@ def pmc_child(args):
     ctx = pkg.Context(pkg.Params.default(), device=0)
     if args.workload == "shard":
         args.batches = 1
-    batches = make_batches(ctx, pkg, args, 0, 1, dev)
+    batches = make_batches(ctx, pkg, args, 0, 1, dev, limit=args.pmc_batches)
     scores = [torch.empty(max(1, d["n_sites"]), dtype=torch.int32, device=dev) for d in batches]
     for _ in range(args.pmc_launches):
         for d, sc in zip(batches, scores):
@@ -230,7 +233,7 @@ def live_counters(args, kernel="ss_score_main"):
                    sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
                    "--c4-scale", str(args.c4_scale), "--chunk", str(args.chunk), "--sites", str(args.sites),
                    "--lt", str(args.lt), "--ln", str(args.ln), "--seed", str(args.seed),
-                   "--pmc-launches", str(args.pmc_launches)]
+                   "--pmc-launches", str(args.pmc_launches), "--pmc-batches", str(args.pmc_batches)]
             # own process group: a pass that overruns is killed with its python child
             proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                     text=True, start_new_session=True)
@@ -273,9 +276,8 @@ def sites_per_launch(args) -> float:
     """Mean sites per launch of the PMC child's workload (rank 0 of one GPU)."""
     if args.workload == "shard":
         return float(args.sites)
-    _, sizes, _ = c4_layout(args.c4_scale, 1)
-    total = sum(sizes)                      # make_batches packs the contigs into full launches
-    return total / -(-total // args.chunk)
+    launches = c4_launches(args.c4_scale, 1, 0, args.chunk)[:args.pmc_batches]
+    return sum(n for pieces in launches for _, _, n in pieces) / len(launches)
 
 
 def cpu_model() -> str:
@@ -296,6 +298,34 @@ def depth_scaled(n: int, lt: float, ln: float) -> int:
     return max(10_000, int(n * 89.1 / max(1.0, lt + ln)))
 
 
+C4_GPUS = 8   # BASELINE.json configs[3]: the 3.2 Gb genome over 8 GPUs
+
+
+def c4_auto_scale(world: int) -> int:
+    """--c4-scale auto: the genome divided so that every GPU holds one eighth of
+    it (8 / N), i.e. exactly configs[3]'s per-GPU share; 1 at N >= 8."""
+    return max(1, -(-C4_GPUS // world))
+
+
+def site_bytes(lt: float, ln: float) -> float:
+    """HBM bytes one resident site takes: its packed reads (4 B each; the
+    generator's mean non-deleted depth is 0.99 (lt + ln), below this bound),
+    two u32 offsets, the ref byte and the i32 score."""
+    return 4.0 * (lt + ln) + 4 + 4 + 1 + 4
+
+
+def c4_rank_bytes(scale: int, world: int, lt: float, ln: float, chunk: int):
+    """Planned resident HBM bytes of each rank's C4 share: its sites, plus the
+    working set of its largest launch (the context's deep lists, 8 B per site,
+    and the generator's depth arrays, 8 B per site)."""
+    _, sizes, plan = c4_layout(scale, world)
+    out = []
+    for p in plan:
+        n = sum(sizes[t] for t in p)
+        out.append(n * site_bytes(lt, ln) + 16.0 * min(chunk, n))
+    return out
+
+
 def c4_layout(scale: int, world: int):
     """Config C4 (BASELINE.json configs[3]): the 24 GRCh38 primary contigs, one
     synthetic site per position, the genome divided by `scale`; contigs are
@@ -308,32 +338,38 @@ def c4_layout(scale: int, world: int):
     return names, sizes, sh.shard_contigs(sizes, world)
 
 
-def make_batches(ctx, pkg, args, rank, world, dev):
+def c4_launches(scale: int, world: int, rank: int, chunk: int):
+    """The rank's contigs back to back (ascending tid), cut into launches of at
+    most `chunk` sites: a launch may hold the end of one contig and the start
+    of the next (sites are independent; fewer, fuller launches).  Each launch
+    is a list of (tid, first position, sites) pieces."""
+    _, sizes, plan = c4_layout(scale, world)
+    launches, cur, room = [], [], chunk
+    for tid in plan[rank]:
+        first = 0
+        while first < sizes[tid]:
+            n = min(room, sizes[tid] - first)
+            cur.append((tid, first, n))
+            first += n
+            room -= n
+            if room == 0:
+                launches.append(cur)
+                cur, room = [], chunk
+    if cur:
+        launches.append(cur)
+    return launches
+
+
+def make_batches(ctx, pkg, args, rank, world, dev, limit=None, scale=None):
     """The rank's HBM-resident synthetic input, generated on the device.
-    c4: every contig of the rank's plan, keyed by (contig, position) -- synth
-    shard = contig index, site = position --, one launch per contig (split into
-    launches of at most --chunk sites).  shard: --batches batches of --sites
-    sites of synth shard = rank."""
+    c4: the launches of c4_launches (genome / `scale`, default --c4-scale),
+    keyed by (contig, position) -- synth shard = contig index, site =
+    position --, the first `limit` of them when given.  shard: --batches
+    batches of --sites sites of synth shard = rank."""
     out = []
     if args.workload == "c4":
-        names, sizes, plan = c4_layout(args.c4_scale, world)
-        # the rank's contigs back to back (ascending tid), cut into launches of
-        # at most --chunk sites: a launch may hold the end of one contig and the
-        # start of the next (sites are independent; fewer, fuller launches)
-        launches, cur, room = [], [], args.chunk
-        for tid in plan[rank]:
-            first = 0
-            while first < sizes[tid]:
-                n = min(room, sizes[tid] - first)
-                cur.append((tid, first, n))
-                first += n
-                room -= n
-                if room == 0:
-                    launches.append(cur)
-                    cur, room = [], args.chunk
-        if cur:
-            launches.append(cur)
-        for pieces in launches:
+        launches = c4_launches(args.c4_scale if scale is None else scale, world, rank, args.chunk)
+        for pieces in launches[:limit]:
             d = synth_pieces(ctx, pkg, args, pieces, dev)
             d.update(tid=pieces[0][0], first=pieces[0][1], pieces=pieces)
             out.append(d)
@@ -412,15 +448,16 @@ def main():
     ap.add_argument("--workload", choices=("c4", "shard"), default="c4",
                     help="c4: GRCh38 contig-sharded genome (BASELINE config C4; strong scaling, total work fixed); "
                          "shard: --sites synthetic sites per rank (weak scaling; the C2/C3/C5 depth runs)")
-    ap.add_argument("--c4-scale", type=int, default=16,
-                    help="C4 genome sites divided by this (3.09e9 / 16 = 1.93e8 sites: fits one GPU at N=1)")
+    ap.add_argument("--c4-scale", type=int, default=None,
+                    help="C4 genome sites divided by this (default: 8 / N, one eighth of the genome per GPU; "
+                         "N = 8 runs the whole 3.09e9-site genome of BASELINE configs[3])")
     ap.add_argument("--chunk", type=int, default=1 << 26,
                     help="c4: most sites per launch (contig pieces packed back to back)")
     ap.add_argument("--sites", type=int, default=1 << 26, help="shard: sites per batch (per step, per GPU)")
     ap.add_argument("--batches", type=int, default=2, help="shard: distinct resident batches cycled per rank")
-    ap.add_argument("--weak-sites", type=int, default=1 << 26,
-                    help="c4: sites per GPU of the secondary weak-scaling line (0 = skip it)")
-    ap.add_argument("--weak-steps", type=int, default=10)
+    ap.add_argument("--strong-scale", type=int, default=16,
+                    help="c4: genome divisor of the secondary strong-scaling line (total work fixed at every N)")
+    ap.add_argument("--strong-steps", type=int, default=10, help="c4: timed steps of that line (0 = skip it)")
     ap.add_argument("--lt", type=float, default=60.0)
     ap.add_argument("--ln", type=float, default=30.0)
     ap.add_argument("--seed", type=int, default=0x5EED5A1DC0FFEE01)
@@ -432,6 +469,7 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 counter passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-launches", type=int, default=3, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-batches", type=int, default=2, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
@@ -441,8 +479,8 @@ def main():
         sys.exit(f"bench.py: refusing to time with tuning/diagnostic variables set: {', '.join(bad)}")
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
-    if args.c4_scale < 1 or args.chunk < 1:
-        sys.exit("bench.py: --c4-scale and --chunk must be >= 1")
+    if (args.c4_scale is not None and args.c4_scale < 1) or args.chunk < 1 or args.strong_scale < 1:
+        sys.exit("bench.py: --c4-scale, --strong-scale and --chunk must be >= 1")
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
             sys.exit(spawn_ranks(args.gpus))      # parent: no torch, no GPU
@@ -476,6 +514,21 @@ def main():
     sharding = importlib.import_module("somatic_sniper_amd.sharding")
     ctx = pkg.Context(pkg.Params.default(), device=local)
     pinned = pkg.model_check()["pinned"]
+    c4 = args.workload == "c4"
+    auto_scale = c4 and args.c4_scale is None
+    planned = None
+    if c4:
+        # every rank resolves the same scale (same world, same device model)
+        _, hbm_total = torch.cuda.mem_get_info(dev)
+        budget = 0.85 * hbm_total
+        if auto_scale:
+            args.c4_scale = c4_auto_scale(world)
+            while max(c4_rank_bytes(args.c4_scale, world, args.lt, args.ln, args.chunk)) > budget:
+                args.c4_scale += 1          # a smaller device than MI355X's 288 GB
+        planned = max(c4_rank_bytes(args.c4_scale, world, args.lt, args.ln, args.chunk))
+        if planned > budget:
+            sys.exit(f"bench.py: --c4-scale {args.c4_scale} needs {planned / 1e9:.1f} GB of HBM per rank, "
+                     f"more than 85% of the device's {hbm_total / 1e9:.1f} GB")
 
     # ---- resident synthetic input (this rank's contigs / shard) ----
     batches = make_batches(ctx, pkg, args, rank, world, dev)
@@ -489,7 +542,6 @@ def main():
     calls = torch.zeros(cap * 28, dtype=torch.uint8, device=dev)
     ncalls = torch.zeros(1, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
-    c4 = args.workload == "c4"
     # a step: c4 scores every batch of the rank (its share of the genome, once);
     # shard scores one batch, cycling through the resident ones
     per_step = list(range(len(batches))) if c4 else None
@@ -541,36 +593,60 @@ def main():
     prop = torch.cuda.get_device_properties(dev)
     me = {"rank": rank, "device": local, "pci_bus_id": getattr(prop, "pci_bus_id", None),
           "ms_per_step": round(rank_elapsed / args.steps * 1e3, 4), "sites": sites_rank,
-          "sites_per_step": sites_step_rank, "launches_per_step": len(per_step) if c4 else 1}
+          "sites_per_step": sites_step_rank, "launches_per_step": len(per_step) if c4 else 1,
+          "hbm_peak_allocated_bytes": torch.cuda.max_memory_allocated(dev)}
     if c4:
         names, sizes, plan = c4_layout(args.c4_scale, world)
         me["contigs"] = [names[t] for t in plan[rank]]
 
-    # ---- secondary weak-scaling line (c4 only): an equal synthetic shard per GPU ----
-    weak = None
-    if c4 and args.weak_sites > 0 and args.weak_steps > 0:
-        wd = ctx.synth_device(pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=1000 + rank), 0,
-                              args.weak_sites, device=dev)
-        wscore = torch.empty(args.weak_sites, dtype=torch.int32, device=dev)
-        wargs = (wd["ref"], wd["off_tumor"], wd["off_normal"], wd["reads_tumor"], wd["reads_normal"])
-        ctx.score_device(*wargs, score=wscore, calls=calls, calls_cap=cap, n_calls=ncalls, stream=stream)
+    # GPU scores the CPU baseline is checked against: the first sites of synth
+    # shard 0 (c4: contig 0, position 0 on; shard: rank 0's batch 0)
+    sample = depth_scaled(2_000_000, args.lt, args.ln) if args.cpu_sample is None else args.cpu_sample
+    pre = None
+    for k, d in enumerate(batches):
+        if d["tid"] == 0 and d["first"] == 0:
+            sample = min(sample, d["n_sites"])
+            pre = score[k][:sample].cpu().numpy()
+    reads_all = float(np.sum(reads))
+    sites_all = sum(d["n_sites"] for d in batches)
+    # free the resident batches before the next line / the counter passes
+    del batches, score
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+
+    # ---- secondary strong-scaling line (c4 only): genome / --strong-scale at every N ----
+    strong = None
+    if c4 and args.strong_steps > 0:
+        sb = make_batches(ctx, pkg, args, rank, world, dev, scale=args.strong_scale)
+        ss = [torch.empty(max(1, d["n_sites"]), dtype=torch.int32, device=dev) for d in sb]
+
+        def strong_step():
+            for d, sc in zip(sb, ss):
+                ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                                 score=sc, calls=calls, calls_cap=cap, n_calls=ncalls, stream=stream)
+        strong_step()
+        torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         w0 = time.perf_counter()
-        for _ in range(args.weak_steps):
-            ctx.score_device(*wargs, score=wscore, calls=calls, calls_cap=cap, n_calls=ncalls, stream=stream)
+        for _ in range(args.strong_steps):
+            strong_step()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
-        w_el, w_sites, w_rate = sharding.aggregate(time.perf_counter() - w0, args.weak_sites * args.weak_steps,
-                                                   world)
+        s_sites = sum(d["n_sites"] for d in sb) * args.strong_steps
+        s_el, s_tot, s_rate = sharding.aggregate(time.perf_counter() - w0, s_sites, world)
         ctx.check()
-        weak = {"value": round(w_rate, 1), "unit": "sites/s", "scaling": "weak",
-                "sites_per_step_per_gpu": args.weak_sites, "steps": args.weak_steps,
-                "ms_per_step": round(w_el / args.weak_steps * 1e3, 4),
-                "workload": f"synthetic shard per GPU (synth shard 1000 + rank), {args.lt:g}xT/{args.ln:g}xN"}
-        del wd, wscore
+        _, s_sizes, _ = c4_layout(args.strong_scale, world)
+        strong = {"value": round(s_rate, 1), "unit": "sites/s", "scaling": "strong", "c4_scale": args.strong_scale,
+                  "genome_sites_per_step": sum(s_sizes), "steps": args.strong_steps,
+                  "ms_per_step": round(s_el / args.strong_steps * 1e3, 4),
+                  "workload": f"C4 / {args.strong_scale} (total work fixed at every N), "
+                              f"{args.lt:g}xT/{args.ln:g}xN, contig-sharded"}
+        del sb, ss
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
 
     if world > 1:
         ranks = [None] * world
@@ -583,12 +659,16 @@ def main():
     avg_kernel_ms = float(np.mean(kms)) if len(kms) else None
     alg_bytes = float(np.mean([bytes_of[k] for k in logged])) if logged else None
     achieved = alg_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms and alg_bytes else None
-    mean_reads = float(np.sum(reads)) / max(1, sum(d["n_sites"] for d in batches))
+    mean_reads = reads_all / max(1, sites_all)
     if c4:
         genome_sites = sum(sizes)
-        config = {"workload": f"C4: synthetic GRCh38 (24 primary contigs, one site per position) / {args.c4_scale}, "
-                              f"{args.lt:g}xT/{args.ln:g}xN Poisson depth, contig-sharded",
+        whole = "the whole genome (BASELINE configs[3])" if args.c4_scale == 1 else f"/ {args.c4_scale}"
+        config = {"workload": f"C4: synthetic GRCh38 (24 primary contigs, one site per position) {whole}, "
+                              f"{args.lt:g}xT/{args.ln:g}xN Poisson depth, contig-sharded over {world} GPU(s)",
                   "genome_sites_per_step": genome_sites, "c4_scale": args.c4_scale,
+                  "c4_scale_mode": ("auto: 8 / N, one eighth of GRCh38 per GPU (per-GPU work fixed)"
+                                    if auto_scale else "fixed (--c4-scale)"),
+                  "planned_hbm_bytes_per_rank": round(planned),
                   "sharding": "sharding.shard_contigs (LPT + local search on the contig lengths)",
                   "plan_imbalance": round(sharding.plan_imbalance(sizes, plan), 5),
                   "contigs_per_rank": [len(p) for p in plan],
@@ -609,7 +689,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong" if c4 else "weak",
+        "scaling": "strong" if c4 and not auto_scale else "weak",
         "vs_baseline": None,
         "dtype": "f32+f64 (u32 packed reads)",
         "data": "synthetic (device-generated counter-based pileups, Poisson depth)",
@@ -629,20 +709,8 @@ def main():
             "launches_timed": len(kms),
         },
     }
-    if weak:
-        result["weak_scaling"] = weak
-    # GPU scores the CPU baseline is checked against: the first sites of synth
-    # shard 0 (c4: contig 0, position 0 on; shard: rank 0's batch 0)
-    sample = depth_scaled(2_000_000, args.lt, args.ln) if args.cpu_sample is None else args.cpu_sample
-    pre = None
-    for k, d in enumerate(batches):
-        if d["tid"] == 0 and d["first"] == 0:
-            sample = min(sample, d["n_sites"])
-            pre = score[k][:sample].cpu().numpy()
-    # free the resident batches before the counter passes start their own copy
-    del batches, score
-    torch.cuda.synchronize(dev)
-    torch.cuda.empty_cache()
+    if strong:
+        result["strong_scaling"] = strong
     if rank == 0 and world == 1 and not args.no_pmc:
         # live counters of the dominant kernel on this same workload (separate
         # rocprofv3 passes after the timed region; MI355X_MICROARCH.md: FETCH_SIZE

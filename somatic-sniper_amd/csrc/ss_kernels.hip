@@ -6,22 +6,25 @@
  * evaluations (sniper_maqcns_glfgen, sniper_maqcns.c:127-248), two consensus
  * calls (sniper_glf2cns, :250-273) and the Phred-space somatic posterior.
  *
- * Work decomposition (DESIGN.md "Kernels"):
- *   ss_score_main   persistent waves walk 16-site blocks.  A block's reads are
- *     staged into LDS by LDS-DMA; per site ONE wave-wide bitonic sort of 16-bit
- *     keys (two per VGPR, both samples) orders the reads, which become 16-bit
- *     fold records written back over the staged reads.  Then two lanes per
- *     (site, sample) run the ordered esum / fsum fold (the reference's float
- *     accumulators fed double increments, sniper_maqcns.c:162-172), split the
- *     10 genotype likelihoods between them, and lane s decides site s (gate,
- *     SNV candidate test, posteriors / joint prior, emit filter).  The DMA of
- *     the next sub-group overlaps the likelihood and decision phases.
- *   ss_score_wide   sites with 513..2048 sort slots (the main kernel lists
- *     them): the same packed network at 1024 / 2048 keys, 16 sites folded and
- *     finished together.
- *   ss_score_deep   one wave per site beyond that (any depth) or with
- *     malformed offsets: counting sort of the order-relevant key fields in
- *     LDS windows, then the same ordered fold, likelihood and decision code.
+ * Work decomposition, one launch = three kernels in order:
+ *   ss_score_main   one LANE per site: a wave walks blocks of 64 consecutive
+ *     sites (grid-strided).  Per lane: the site's packed reads (x4 loads into
+ *     registers) become 16-bit order keys in a 128-element bitonic network in
+ *     registers (two keys per VGPR, packed min / max), the sorted keys become
+ *     8-bit fold records in LDS, then the ordered esum / fsum fold (the
+ *     reference's float accumulators fed double increments,
+ *     sniper_maqcns.c:162-172), the 10 genotype likelihoods, glf2cns and the
+ *     site decision (gate, SNV candidate test, posteriors / joint prior, emit
+ *     filter), all inside the lane.  Sites past the network (> 128 reads in a
+ *     sample), with a read of minq >= 64 or malformed offsets are listed.
+ *   ss_score_group  the listed sites with at most 2048 reads per sample: per
+ *     (site, sample) a unit of 1..16 lanes sorts 128 keys per lane as above
+ *     and merges across lanes (DPP); 16 sites are folded two lanes per
+ *     (site, sample) and finished together.
+ *   ss_score_deep   one wave per site beyond that (any depth), with a wild
+ *     read or malformed offsets: counting sort of the order-relevant key
+ *     fields in LDS windows, then the same ordered fold, likelihood and
+ *     decision code.
  *
  * Bit-exactness: built with -ffp-contract=off (no FMA contraction); float
  * division and double sqrt are correctly rounded (sqrt re-checked with fma);
@@ -34,7 +37,6 @@
 /* Fixed tuning of the shipped kernels (each measured on MI355X):
  * one code path per choice, no run-time or build-time alternatives. */
 #define SS_FOLD_UNROLL 8  /* fold loop unroll (2 -> 8: +0.5% main, +4% at 500x/500x) */
-#define SS_PRIO_WIDE 1    /* the same over the wide kernel's network (+3.7% at 500x/500x) */
 /* `#pragma unroll N` with N from a macro: the count reaches the pragma expanded */
 #define SS_PRAGMA(x) _Pragma(#x)
 #define SS_UNROLL(n) SS_PRAGMA(unroll n)
@@ -49,19 +51,6 @@ __device__ __forceinline__ void wave_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-}
-
-/* Sum over the 64 lanes with DPP row shifts + row broadcasts (no LDS
- * round trip); the total ends in lane 63 and is returned wave-uniform. */
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); /* row_shr:1 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); /* row_shr:2 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); /* row_shr:4 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); /* row_shr:8 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); /* row_bcast:15 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); /* row_bcast:31 */
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 struct SlotRes {
@@ -332,7 +321,8 @@ __device__ __forceinline__ void glf_and_cns(int q, const float es[4], const floa
 }
 
 /* qAdd (somatic_sniper.c:18) with the out-of-range index clamped + counted */
-__device__ __forceinline__ int qadd(const int32_t *T, int x, int y, int &clamped)
+template <typename TT>
+__device__ __forceinline__ int qadd(const TT *T, int x, int y, int &clamped)
 {
     int idx = 512 + y - x;
     if (idx < 0) { idx = 0; ++clamped; }
@@ -345,7 +335,8 @@ __device__ __forceinline__ bool proper_subset(int a, int b) { return b != a && (
 /* --------------------------------------------------------------------------
  * Phase D: the site decision of glf_somatic (somatic_sniper.c:117-273).
  * ------------------------------------------------------------------------ */
-__device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc,
+template <typename TT>
+__device__ void decide_site(const ss_score_args &a, const TT *QT, uint32_t site, uint32_t refc,
                             const SlotRes &rt, const SlotRes &rn)
 {
     const ss_dev_model &m = a.m;
@@ -377,15 +368,15 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
                 int v = (int)rn.lk[i] + (int)rt.lk[j] + ss_tab_jprior(m)[(rb4 * 10 + i) * 10 + j];
                 if (v > 255) v = 255;
                 if (v < best) { best = v; bi = i; bj = j; }
-                marg = qadd(ss_tab_qadd(m), marg, v, clamped);
+                marg = qadd(QT, marg, v, clamped);
             }
 #pragma unroll 1
         for (int j = 0; j < 10; ++j) {
             int v = (int)rn.lk[j] + (int)rt.lk[j] + ss_tab_jprior(m)[(rb4 * 10 + j) * 10 + j];
             if (v > 255) v = 255;
             const int l = v - marg;
-            qps = qadd(ss_tab_qadd(m), qps, l, clamped);
-            if (j != bj) jcq = qadd(ss_tab_qadd(m), jcq, l, clamped);  /* stale-index quirk, :196 */
+            qps = qadd(QT, qps, l, clamped);
+            if (j != bj) jcq = qadd(QT, jcq, l, clamped);  /* stale-index quirk, :196 */
         }
         if (jcq > 255) jcq = 255;
         /* glfBase (somatic_sniper.c:26): genotype index -> nt16 bit set */
@@ -402,8 +393,8 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
         for (int j = 0; j < 10; ++j) {
             const int xt = (int)rt.lk[j] + ss_tab_prior(m)[rb4 * 10 + j];
             const int xn = (int)rn.lk[j] + ss_tab_prior(m)[rb4 * 10 + j];
-            st = qadd(ss_tab_qadd(m), xt, st, clamped);
-            sn = qadd(ss_tab_qadd(m), xn, sn, clamped);
+            st = qadd(QT, xt, st, clamped);
+            sn = qadd(QT, xn, sn, clamped);
         }
 #pragma unroll 1
         for (int j = 0; j < 10; ++j) {
@@ -411,7 +402,7 @@ __device__ void decide_site(const ss_score_args &a, uint32_t site, uint32_t refc
             int vn = (int)rn.lk[j] + ss_tab_prior(m)[rb4 * 10 + j] - sn;
             if (vt > 255) vt = 255;
             if (vn > 255) vn = 255;
-            qps = qadd(ss_tab_qadd(m), qps, vt + vn, clamped);
+            qps = qadd(QT, qps, vt + vn, clamped);
         }
     }
     a.score[site] = qps;
@@ -457,19 +448,22 @@ __device__ __forceinline__ void store_glf(ss_glf_t *dst, uint32_t ref16, const u
 }
 
 /* --------------------------------------------------------------------------
- * Wave-parallel site machinery of the wide kernel (sites past the main
- * kernel's per-lane network): 16-bit order keys, the packed
- * wave-wide bitonic network, 8-bit fold records, the two-lane ordered fold
- * and the sub-group finish (likelihoods, quantisation, decision).
+ * Shared machinery of the lane-group kernel (sites past the main kernel's
+ * per-lane network): 8-bit fold records, packed u16 min / max,
+ * cross-lane exchanges, the two-lane ordered fold and the sub-group finish
+ * (likelihoods, quantisation, decision).
  *
- * 16-bit order key of a read (read_key16):
+ * 16-bit order key of a read (ln_chunk builds it):
  *   sample<<15 | base<<13 | minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz
+ * E = baseQ >> 6 and nz = (baseQ & 0x3f) != 0 order the reads of one
+ * (minq < 4, hasbase, strand) class exactly as the reference's baseQ
+ * tie-break does as far as the clamp of sniper_maqcns.c:165 is concerned.
  * Inside one (sample, base) group the reference's descending key walk
  * (sniper_maqcns.c:157-172) visits elements in exactly this order up to swaps
  * of elements with identical (q, strand), which leave every float sum
  * unchanged.
  * ------------------------------------------------------------------------ */
-#define GB 16               /* sites per wide-kernel sub-group */
+#define GB 16               /* sites per group-kernel sub-group */
 
 struct Slot3 {
     uint32_t rec_n;      /* u32 index of the fold records | non-deleted depth << 16 */
@@ -479,37 +473,7 @@ struct Slot3 {
 };
 
 
-/* 16-bit order key (see the section comment); 0xffff = no contribution or pad.
- *   sample<<15 | base<<13 | minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz
- * E = baseQ >> 6 and nz = (baseQ & 0x3f) != 0 order the reads of one
- * (minq < 4, hasbase, strand) class exactly as the reference's baseQ tie-break
- * does as far as the clamp of sniper_maqcns.c:165 is concerned (classes
- * 1..63 | 64 | 65..127 | 128 | ...); for minq >= 4 they only reorder reads with
- * identical (q, strand), which leaves every sum unchanged.
- * base / hasbase come from two per-site tables with 2-bit fields indexed by
- * 2*nt16 (entry 0, '=', already resolved to the reference base):
- * tb = base, th = hasbase; see nt_tables(). */
-__device__ __forceinline__ uint32_t read_key16(uint32_t rd, uint32_t tb, uint32_t th,
-                                               uint32_t samplebit)
-{
-    const uint32_t minq = min(rd & 0xffu, (rd >> 8) & 0xffu);
-    const uint32_t lo6 = rd & 0x3f00u;
-    const uint32_t nz = lo6 != 0u ? 1u : 0u;
-    const uint32_t nt2 = (rd >> 15) & 0x1eu;
-    const uint32_t base = __builtin_amdgcn_ubfe(tb, nt2, 2u);
-    const uint32_t hb = __builtin_amdgcn_ubfe(th, nt2, 1u);
-    const uint32_t E = __builtin_amdgcn_ubfe(rd, 14u, 2u);
-    const uint32_t st = __builtin_amdgcn_ubfe(rd, 20u, 1u);
-    const uint32_t key = samplebit | base << 13 | minq << 5 | hb << 4 | st << 3 | E << 1 | nz;
-    /* a contributing normal read can have every field at its maximum (mapQ =
-     * baseQ = 255, T, reverse): 0xfffe keeps it below the pad key, and for
-     * minq >= 4 the E / nz bits only order reads of equal (q, strand).  A read
-     * with clamped q = 0 gets 0xffff: an OR with the mask rather than a select,
-     * which the compiler turned into a branch around the key arithmetic. */
-    return min(key, 0xfffeu) | ((minq | lo6) != 0u ? 0u : 0xffffu);
-}
-
-/* per-site base tables of read_key16 (bam_nt16_nt4_table semantics,
+/* per-site base tables of the deep kernel's bins (bam_nt16_nt4_table semantics,
  * sniper_maqcns.c:19,153-154: single-base codes -> 0..3 with hasbase, every
  * other code counts as A without hasbase; code 0 '=' -> the reference base). */
 __device__ __forceinline__ void nt_tables(uint32_t ref16, uint32_t &tb, uint32_t &th)
@@ -518,30 +482,6 @@ __device__ __forceinline__ void nt_tables(uint32_t ref16, uint32_t &tb, uint32_t
     constexpr uint32_t TH = 1u << 2 | 1u << 4 | 1u << 8 | 1u << 16;
     tb = TB | ((TB >> (2u * ref16)) & 3u);
     th = TH | ((TH >> (2u * ref16)) & 1u);
-}
-
-/* 8-bit fold record (wide kernel: twice the sites of a 16-bit record in the
- * same LDS arena, so a sub-group fills the 16 sites of the fold), for sites
- * whose contributing reads all have minq < 64 (wide_q_fits):
- *   bits 0..5 q | bit 6 strand | bit 7 1 (fsum multiplier);
- * (r >> 2) & 16 is strand << 4 like the u32 record's top byte. */
-__device__ __forceinline__ uint32_t key_to_rec8(uint32_t k)
-{
-    const uint32_t q = max((k >> 5) & 0xffu, (k & 1u) << 2);
-    return q | (k & 8u) << 3 | 1u << 7;
-}
-
-/* every contributing key of the lane's registers has minq < 64 (key bits 11, 12 clear) */
-template <int K>
-__device__ __forceinline__ bool wide_q_fits(const uint32_t (&v)[1][K])
-{
-    bool ok = true;
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-        const uint32_t lo = v[0][r] & 0xffffu, hi = v[0][r] >> 16;
-        ok = ok && (lo == 0xffffu || (lo & 0x1800u) == 0u) && (hi == 0xffffu || (hi & 0x1800u) == 0u);
-    }
-    return ok;
 }
 
 template <typename RecT> struct RecForm;
@@ -577,14 +517,6 @@ __device__ __forceinline__ uint32_t pk_max_swo(uint32_t x, uint32_t o)
     asm("v_pk_max_u16 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(x), "v"(o));
     return r;
 }
-/* halfswap(max(x, halfswap(o))) = max(halfswap(x), o) */
-__device__ __forceinline__ uint32_t pk_max_swx(uint32_t x, uint32_t o)
-{
-    uint32_t r;
-    asm("v_pk_max_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(x), "v"(o));
-    return r;
-}
-
 /* x from lane ^ LJ: DPP quad permutes for 1 and 2, bank-masked DPP row
  * shifts for 4 and 8, ds_swizzle for 16 and 31, v_permlane32_swap for 32,
  * DPP mirrors for 3, 7 and 15. */
@@ -624,205 +556,6 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
         return xor_lane<32>(xor_lane<31>(x));
     }
 }
-
-/* Cross-lane compare-exchange of packed u16 pairs: lanes with bit LJ clear
- * keep min(x, o), lanes with it set keep max(x, o).  (An exec-masked max,
- * 2 VALU instead of 3, measured slower: SALU exec writes.) */
-template <int LJ>
-__device__ __forceinline__ uint32_t cx_lanes(uint32_t x, uint32_t o)
-{
-    return (lane_id() & (uint32_t)LJ) ? pk_max(x, o) : pk_min(x, o);
-}
-
-/* In-register compare-exchange of the two halves: lo = min, hi = max, by two
- * SDWA word ops instead of swap + min + max + merge.  The second op reads the
- * first one's result through dst_unused:UNUSED_PRESERVE; back to back that
- * read is stale on gfx950 (measured), so either one independent instruction
- * (cx_halves2: two registers interleaved) or one wait state separates them. */
-__device__ __forceinline__ void cx_halves2(uint32_t &x0, uint32_t &x1)
-{
-    uint32_t r0, r1;
-    asm volatile("v_max_u16_sdwa %0, %2, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
-                 "v_max_u16_sdwa %1, %3, %3 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1\n\t"
-                 "v_min_u16_sdwa %0, %2, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1\n\t"
-                 "v_min_u16_sdwa %1, %3, %3 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1"
-                 : "=&v"(r0), "=&v"(r1)
-                 : "v"(x0), "v"(x1));
-    x0 = r0;
-    x1 = r1;
-}
-
-/* cx_halves over every register of the M x K set, two at a time */
-template <int M, int K>
-__device__ __forceinline__ void halves_all(uint32_t (&v)[M][K])
-{
-    constexpr int N = M * K;
-#pragma unroll
-    for (int i = 0; i + 1 < N; i += 2) cx_halves2(v[i / K][i % K], v[(i + 1) / K][(i + 1) % K]);
-    static_assert((N & 1) == 0, "registers come in pairs");
-}
-
-/* half cleaners e <-> e ^ j for j = J, J/2, ..., 1 (compile-time recursion);
- * M independent networks are advanced together so their dependency chains
- * (and DPP wait states) interleave. */
-template <int M, int K, uint32_t J>
-__device__ __forceinline__ void half_clean(uint32_t (&v)[M][K])
-{
-    constexpr uint32_t E = 2u * K;
-    if constexpr (J == 0) {
-        return;
-    } else {
-        if constexpr (J >= E) {
-            constexpr uint32_t lj = J / E;
-#pragma unroll
-            for (int m = 0; m < M; ++m)
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    const uint32_t o = xor_lane<(int)lj>(v[m][r]);
-                    v[m][r] = cx_lanes<(int)lj>(v[m][r], o);
-                }
-        } else if constexpr (J >= 2u) {
-#pragma unroll
-            for (int m = 0; m < M; ++m)
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    const int r2 = r ^ (int)(J >> 1);
-                    if (r2 > r) {
-                        const uint32_t mn = pk_min(v[m][r], v[m][r2]), mx = pk_max(v[m][r], v[m][r2]);
-                        v[m][r] = mn;
-                        v[m][r2] = mx;
-                    }
-                }
-        } else {
-            halves_all<M, K>(v);
-        }
-        half_clean<M, K, (J >> 1)>(v);
-    }
-}
-
-/* Bitonic sort (the "flip" formulation: every comparator puts the minimum at
- * the lower index, so all directions are single lane bits), ascending, of
- * 128*K u16 keys: element e = lane*2K + 2r + h lives in half h of v[m][r]. */
-template <int M, int K, uint32_t k>
-__device__ __forceinline__ void flip_stage(uint32_t (&v)[M][K])
-{
-    constexpr uint32_t E = 2u * K;
-    /* mirror: e <-> e ^ (k-1) */
-    if constexpr (k == 2) {
-        halves_all<M, K>(v);                              /* e <-> e ^ 1: the two halves */
-    } else if constexpr (k <= E) {
-#pragma unroll
-        for (int m = 0; m < M; ++m)
-#pragma unroll
-            for (int r = 0; r < K; ++r) {
-                const int r2 = ((2 * r) ^ (int)(k - 1)) >> 1;
-                if (r2 > r) {
-                    const uint32_t mn = pk_min_swo(v[m][r], v[m][r2]);
-                    const uint32_t mx = pk_max_swx(v[m][r], v[m][r2]);
-                    v[m][r] = mn;
-                    v[m][r2] = mx;
-                }
-            }
-    } else {
-        constexpr uint32_t mx_lane = k / E - 1u;          /* lane xor of the mirror */
-        constexpr int lbit = (int)((mx_lane + 1u) >> 1);    /* lanes with it set keep the max */
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            uint32_t nv[K];
-#pragma unroll
-            for (int r = 0; r < K; ++r) {
-                const uint32_t o = xor_lane<(int)mx_lane>(v[m][K - 1 - r]);    /* halves swapped in the op */
-                const uint32_t hi = pk_max_swo(v[m][r], o), lo = pk_min_swo(v[m][r], o);
-                nv[r] = (lane_id() & (uint32_t)lbit) ? hi : lo;
-            }
-#pragma unroll
-            for (int r = 0; r < K; ++r) v[m][r] = nv[r];
-        }
-    }
-    half_clean<M, K, (k >> 2)>(v);
-}
-
-/* level k of the network; the top level (k = 128K, the merge of the two
- * halves) only when `top` (wave-uniform) */
-template <int M, int K, uint32_t k>
-__device__ __forceinline__ void flip_level(uint32_t (&v)[M][K], bool top)
-{
-    if constexpr (k < 128u * K) flip_stage<M, K, k>(v);
-    else if constexpr (k == 128u * K) { if (top) flip_stage<M, K, k>(v); }
-}
-
-template <int M, int K>
-__device__ __forceinline__ void packed_bitonic_flip(uint32_t (&v)[M][K], bool top = true)
-{
-    static_assert(K == 1 || K == 2 || K == 4 || K == 8 || K == 16, "sort size");
-    flip_level<M, K, 2>(v, top);
-    flip_level<M, K, 4>(v, top);
-    flip_level<M, K, 8>(v, top);
-    flip_level<M, K, 16>(v, top);
-    flip_level<M, K, 32>(v, top);
-    flip_level<M, K, 64>(v, top);
-    flip_level<M, K, 128>(v, top);
-    flip_level<M, K, 256>(v, top);
-    flip_level<M, K, 512>(v, top);
-    flip_level<M, K, 1024>(v, top);
-    flip_level<M, K, 2048>(v, top);
-}
-
-/* Split placement.  Every normal key carries the sample bit, so when each
- * sample fits in half of the network (nt, nn <= 64K) and the normal reads go
- * to network elements 64K.. (lanes 32..63), the levels below the top leave the
- * array [tumor sorted, pads | normal sorted, pads]: each sample sorted in its
- * half, and the top merge level (7 of the 28 comparator stages at K = 1) is
- * skipped.  The normal run then starts at element 64K instead of c4. */
-template <int K>
-__device__ __forceinline__ bool split_fits(uint32_t nt, uint32_t nn)
-{
-    return nt <= 64u * K && nn <= 64u * K;
-}
-
-/* Group sizes (sample, base) do not depend on the order, so they are counted
- * from the keys before the sort, next to the rms sums: each contributing key
- * adds one to its base's field of a per-lane counter (8-bit fields when a
- * sample has at most 128 sort slots, K = 1; else 16-bit fields, two words),
- * and one wave reduction per word replaces the eight ballot-and-popcount
- * boundary counts over the sorted network. */
-template <int K>
-struct GroupCount {
-    static constexpr bool NARROW = K == 1;
-    static constexpr int NW = NARROW ? 1 : 2;
-    uint32_t t[NW], n[NW];        /* per-lane partial counts: tumor, normal */
-    __device__ __forceinline__ void zero()
-    {
-#pragma unroll
-        for (int i = 0; i < NW; ++i) t[i] = n[i] = 0u;
-    }
-    /* the lane's key pair (k0, k1) of one sample; 0xffff (pad or q = 0) adds nothing */
-    __device__ __forceinline__ void add(uint32_t k0, uint32_t k1, bool tum)
-    {
-        uint32_t inc[NW];
-        if constexpr (NARROW) {
-            inc[0] = (k0 != 0xffffu ? 1u << ((k0 >> 10) & 0x18u) : 0u) +      /* 8 * base */
-                     (k1 != 0xffffu ? 1u << ((k1 >> 10) & 0x18u) : 0u);
-        } else {
-            const uint32_t o0 = k0 != 0xffffu ? 1u << ((k0 >> 9) & 16u) : 0u; /* 16 * (base & 1) */
-            const uint32_t o1 = k1 != 0xffffu ? 1u << ((k1 >> 9) & 16u) : 0u;
-            const bool h0 = (k0 >> 14) & 1u, h1 = (k1 >> 14) & 1u;
-            inc[0] = (h0 ? 0u : o0) + (h1 ? 0u : o1);
-            inc[1] = (h0 ? o0 : 0u) + (h1 ? o1 : 0u);
-        }
-#pragma unroll
-        for (int i = 0; i < NW; ++i) {
-            t[i] += tum ? inc[i] : 0u;
-            n[i] += tum ? 0u : inc[i];
-        }
-    }
-    /* base b's count from reduced words */
-    static __device__ __forceinline__ uint32_t field(const uint32_t *w, int b)
-    {
-        if constexpr (NARROW) return (w[0] >> (8 * b)) & 0xffu;
-        else return (w[b >> 1] >> (16 * (b & 1))) & 0xffffu;
-    }
-};
 
 /* Fold of one (site, sample) by TWO lanes: role 0 accumulates esum, role 1
  * fsum (sniper_maqcns.c:165-172).  Both run the same instruction stream:
@@ -896,16 +629,19 @@ __device__ __forceinline__ void fold_sample(const RecT *rec, const uint32_t cnt[
     }
 }
 
+/* Maximum over the 64 lanes with DPP row shifts + row broadcasts, returned
+ * wave-uniform (an SGPR): no LDS permute and no per-lane permute addresses
+ * held in VGPRs across the main kernel's block loop.  Lanes whose DPP source
+ * lies outside the row keep `old` = 0, the identity of an unsigned max. */
 __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
-}
-
-__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l)
-{
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false)); /* row_shr:1 */
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false)); /* row_shr:2 */
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false)); /* row_shr:4 */
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false)); /* row_shr:8 */
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false)); /* row_bcast:15 */
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false)); /* row_bcast:31 */
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 /* Phases B, C, D for the G sites of a sub-group.  Fold records are RecT
@@ -928,11 +664,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         depth = m3.rec_n >> 16;
         rms = m3.rms;
         const RecT *rec = recs + (m3.rec_n & 0xffffu);
-#ifndef SS_AB_WNOFOLD
         fold_sample<RecT>(rec, cnt, fk, role, acc);
-#else
-        for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b] + (float)rec[b];
-#endif
     } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
@@ -950,11 +682,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     uint32_t c[4];
     const uint32_t tot = rescale_counts(cnt, c);
     float mine[5];
-#ifndef SS_AB_WNOFIN
     geno_p5(role, es, fs, c, tot, a.m, mine);
-#else
-    for (int t = 0; t < 5; ++t) mine[t] = es[t & 3] + (float)c[t & 3];
-#endif
 #pragma unroll
     for (int t = 0; t < 5; ++t) mine[t] = act ? mine[t] : 0.0f;
     float p[10];
@@ -982,7 +710,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     }
     wave_sync();
     /* the decision reads both samples' records straight from LDS */
-    if ((int)lane < G) decide_site(a, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
+    if ((int)lane < G) decide_site(a, ss_tab_qadd(a.m), sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
     wave_sync();
 }
 
@@ -995,7 +723,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
  * and the blocks are grid-strided.  Everything per site runs inside its lane,
  * serially, so one VALU instruction advances 64 sites:
  *   1. key build: the site's packed reads (x4 loads straight into registers)
- *      become 16-bit order keys (read_key16) in a per-lane bitonic network of
+ *      become 16-bit order keys (see above) in a per-lane bitonic network of
  *      LN_N elements; the rms sums and the group sizes (contributing reads per
  *      (sample, base)) are accumulated on the way.
  *   2. sort: the network, in registers, two keys per register: every
@@ -1157,10 +885,6 @@ __device__ __forceinline__ void ln_load(const LaneIn &in, uint32_t c, uint32_t (
 {
     const bool fa = c < in.nca;
     const uint32_t *src = (fa ? in.pa : in.pb) + 4u * c;
-#ifdef SS_AB_NOLOAD
-    for (int t = 0; t < 4; ++t) x[t] = ((in.na + 4u * c + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;
-    return;
-#endif
     if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */
         const int lim = (int)(fa ? in.na : in.nab) - (int)(4u * c);
 #pragma unroll
@@ -1468,7 +1192,11 @@ void ss_score_main(ss_score_args a)
     __shared__ double fk[LN_FK_ZERO + 1];
     __shared__ uint2 lut[LN_LUT_BYTES / 8];
     __shared__ LaneLds LL[LN_WAVES];
+    /* qAddTable (somatic_sniper.c:13,101-107) in LDS as int16 (its entries lie
+     * in [-512, 0]; 2 KB keeps 3 workgroups per CU within 160 KB) */
+    __shared__ int16_t qtab[1024];
     for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < 256u ? ss_tab_fk(a.m)[i] : 0.0;
+    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) qtab[i] = (int16_t)ss_tab_qadd(a.m)[i];
     ln_lut_build(lut);
     __syncthreads();
     const uint32_t lane = lane_id();
@@ -1513,6 +1241,9 @@ void ss_score_main(ss_score_args a)
             in.na4 = ok ? (nrm ? nn4 : nt4) : 0u;
             in.nb = joint && ok ? nn : 0u;
             in.nca = in.na4 >> 2;
+            /* opaque: otherwise the chunk tests c < nca become 4c < na4, whose
+             * constants 68 .. 124 are not inline and took 16 SGPRs */
+            asm("" : "+v"(in.nca));
             in.nab = in.na4 + in.nb;
             const uint32_t ob = ok ? on : 0u;
             in.pa = (nrm ? a.reads_n : a.reads_t) + (ok ? (nrm ? on : ot) : 0u);
@@ -1526,12 +1257,8 @@ void ss_score_main(ss_score_args a)
             const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
             /* a read of minq >= 64 needs 16-bit records: the wide kernel */
             wild = wild || acc.maxq >= 64u;
-#ifndef SS_AB_NONET                 /* SS_AB_*: phase ablations for timing (tools/ab.sh), never shipped */
             ln_levels<LN_R, 2>(v);
-#endif
-#ifndef SS_AB_NOREC
             ln_records(v, 4u * nch, L, lane);
-#endif
             /* fold and finish the pass's samples: A (its records from 0), then
              * in joint mode B (after A's contributing reads) */
             const uint32_t ca = acc.cnt_a;
@@ -1540,17 +1267,9 @@ void ss_score_main(ss_score_args a)
                 const bool smpN = nrm || k == 1u;
                 float es[4], fs[4];
                 uint32_t c[4];
-#ifndef SS_AB_NOFOLD
                 ln_fold(L, lane, k ? tot_a : 0u, k ? acc.cnt_b : acc.cnt_a, fk, es, fs, c);
-#else
-                for (int b = 0; b < 4; ++b) { es[b] = fs[b] = (float)(acc.cnt_a >> b); c[b] = (acc.cnt_a >> (8 * b)) & 0xffu; }
-#endif
                 uint32_t l03, l47, l89, cn, mq;
-#ifndef SS_AB_NOFIN
                 ln_finish(es, fs, c, smpN ? nn : nt, k ? acc.rms_b : acc.rms_a, a.m, l03, l47, l89, cn, mq);
-#else
-                l03 = __float_as_uint(es[0]); l47 = __float_as_uint(fs[1]); l89 = c[2]; cn = 0x11000000u; mq = c[3];
-#endif
                 if (smpN) {
                     lkN03 = l03; lkN47 = l47; lkN89 = l89; cnsN = cn; mqN = mq;
                 } else {
@@ -1589,11 +1308,7 @@ void ss_score_main(ss_score_args a)
             }
         }
         wave_sync();
-#ifndef SS_AB_NODECIDE
-        if (ok) decide_site(kernarg_args(), s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
-#else
-        if (ok) a.score[s] = (int)L.res[lane][0].cns;
-#endif
+        if (ok) decide_site(kernarg_args(), qtab, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
         wave_sync();
     }
     if (lane == 0 && ndeep) {
@@ -1606,373 +1321,11 @@ void ss_score_main(ss_score_args a)
     }
 }
 
-/* --------------------------------------------------------------------------
- * Wide kernel: the sites the main kernel left on the deep list (more than
- * PK_MAX sort slots, e.g. 500x/500x panels) whose samples have at most
- * SS_WIDE_MAXSLOTS reads each.
- *
- * One workgroup per CU, SS_WIDE_BLOCK / 64 independent waves sharing 144 KB
- * of LDS as per-wave arenas of 8-bit fold records.  A wave takes 16 list
- * entries at a time and, sort unit by sort unit, loads the packed reads
- * straight from HBM into registers, sorts them with the same packed bitonic
- * network as the main kernel (1024 or 2048 keys: K = 8 or 16 registers), and
- * writes the fold records into the arena.  A unit is a whole site of at most
- * SS_WIDE_MAXSLOTS sort slots (both samples in one network), else one of its
- * samples (1200x/1000x panels; also past 1024 slots when one sample has at
- * most 512 reads: K = 4 + K = 8 instead of one 2048-key network).  Then the sites are folded together -- lane =
- * (site, sample, role), so the wave runs up to 64 serial chains at once
- * instead of one -- and finished by the main kernel's code.  Larger or
- * malformed sites, and sites with a read of minq >= 64, go to the second
- * deep list (ss_score_deep).
- * ------------------------------------------------------------------------ */
-namespace {
-
-#define WIDE_WAVES (SS_WIDE_BLOCK / 64)
-#define WIDE_LDS_REC (WIDE_WAVES == 8 ? 147456 : 12064 * 12)   /* u8 fold records per workgroup: 141-144 KB */
-#define WIDE_ARENA (WIDE_LDS_REC / WIDE_WAVES)      /* per wave (< 2^16: Slot3 rec_n) */
-
-struct alignas(16) WideLds {
-    uint8_t arena[WIDE_WAVES][WIDE_ARENA];
-    Slot3    slot[WIDE_WAVES][2 * GB];
-    SlotRes  res[WIDE_WAVES][2 * GB];
-    uint32_t site[WIDE_WAVES][GB];
-    uint32_t refc[WIDE_WAVES][GB];
-};
-
-/* A wide site's packed reads in the sort placement (tumor [0, nt), normal
- * [ntr, ntr + nn)): element pair (e0, e0 + 1), e0 = 2 * (r * 64 + lane), in
- * rd[2r], rd[2r + 1]; 0 (no contribution) outside the site.  Issued one site
- * ahead of its sort so the HBM latency overlaps the previous site's work. */
-struct WideSite {
-    uint32_t ot, nt, on, nn;
-    uint32_t ref;      /* ref char | nt16 code << 8, loaded with the offsets (one site ahead) */
-    uint32_t unit;     /* 0 the whole site, 1 its tumor, 2 its normal (see wide_place) */
-    uint32_t sp;       /* non-split placement: elements below sp are tumor reads, the rest normal */
-    bool split;        /* unit 0, split placement (see split_fits): top level skipped */
-    bool over;         /* a sample beyond SS_WIDE_MAXSLOTS reads or malformed offsets: deep kernel */
-};
-
-__device__ __forceinline__ void wide_place(WideSite &w, uint32_t end_t, uint32_t end_n)
-{
-    w.over = max(w.nt, w.nn) > SS_WIDE_MAXSLOTS ||
-             w.ot + w.nt < w.ot || w.ot + w.nt > end_t || w.on + w.nn < w.on || w.on + w.nn > end_n;
-    const uint32_t slots = w.nt + (w.nt & 1u) + w.nn;
-    /* past 1024 slots with one sample of at most 512 reads: a 512-key and a
-     * 1024-key network (45 x 4 + 55 x 8 register stages) instead of one split
-     * 2048-key network (55 x 16) */
-    const bool small_unit = slots > 1024u && max(w.nt, w.nn) <= 1024u && min(w.nt, w.nn) <= 512u;
-    w.unit = !w.over && (slots > SS_WIDE_MAXSLOTS || small_unit) ? 1u : 0u;
-    w.sp = w.unit ? 0xffffu : w.nt + (w.nt & 1u);
-    const bool k8 = slots <= 1024u;                          /* the network sort_site_wide picks */
-    w.split = !w.unit && (k8 ? split_fits<8>(w.nt, w.nn) : split_fits<16>(w.nt, w.nn));
-}
-
-/* the normal unit of a site whose tumor unit w was */
-__device__ __forceinline__ WideSite wide_normal_unit(WideSite w)
-{
-    w.unit = 2u;
-    w.sp = 0u;
-    return w;
-}
-
-/* network size of a unit: reads it sorts (incl. the pad between samples) */
-__device__ __forceinline__ uint32_t wide_unit_slots(const WideSite &w)
-{
-    return w.unit == 0u ? w.nt + (w.nt & 1u) + w.nn : (w.unit == 1u ? w.nt : w.nn);
-}
-
-/* All 16 register pairs, whatever the site's network: choosing 8 or 16 by a
- * branch put rd in scratch (measured 30% slower).  One base pointer and
- * limit per lane (split) or two (otherwise): 5% faster at 500x/500x than a
- * per-pair select of sample, index and pointer. */
-__device__ __forceinline__ void wide_load(const ss_score_args &a, const WideSite &w, uint32_t (&rd)[32])
-{
-    const uint32_t lane = lane_id();
-    if (w.split) {
-        /* lanes 0..31 the tumor, 32..63 the normal: one base pointer per lane */
-        const bool tl = lane < 32u;
-        const uint32_t *bp = tl ? a.reads_t + w.ot : a.reads_n + w.on;
-        const uint32_t lim = w.over ? 0u : (tl ? w.nt : w.nn);
-        const uint32_t i00 = (lane & 31u) * 2u;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t i0 = i00 + (uint32_t)r * 64u;
-#ifndef SS_AB_WNOLOAD
-            rd[2 * r] = i0 < lim ? __builtin_nontemporal_load(bp + i0) : 0u;
-            rd[2 * r + 1] = i0 + 1u < lim ? __builtin_nontemporal_load(bp + i0 + 1) : 0u;
-#else
-            rd[2 * r] = i0 < lim ? ((i0 * 0x9E3779B1u) & 0x001f3f3fu) : 0u;
-            rd[2 * r + 1] = i0 + 1u < lim ? (((i0 + 1u) * 0x9E3779B1u) & 0x001f3f3fu) : 0u;
-#endif
-        }
-    } else {
-        /* element e: tumor read e below sp, normal read e - sp above (a
-         * unit takes one sample: sp past every element, or 0).  The normal
-         * base is offset by -sp so that element e indexes it directly; for a
-         * tumor unit it is never dereferenced. */
-        const uint32_t sp = w.sp;
-        const uint32_t *tp = a.reads_t + w.ot, *np = a.reads_n + w.on - sp;
-        const uint32_t lt = w.over ? 0u : w.nt, ln = w.over ? 0u : sp + w.nn;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;            /* as in sort_sites */
-            const bool tum = e0 < sp;
-            const uint32_t *src = (tum ? tp : np) + e0;
-            const uint32_t lim = tum ? lt : ln;
-#ifndef SS_AB_WNOLOAD
-            rd[2 * r] = e0 < lim ? __builtin_nontemporal_load(src) : 0u;
-            rd[2 * r + 1] = e0 + 1u < lim ? __builtin_nontemporal_load(src + 1) : 0u;
-#else
-            rd[2 * r] = e0 < lim ? ((e0 * 0x9E3779B1u) & 0x001f3f3fu) : 0u;
-            rd[2 * r + 1] = e0 + 1u < lim ? (((e0 + 1u) * 0x9E3779B1u) & 0x001f3f3fu) : 0u;
-#endif
-        }
-    }
-}
-
-/* Returns the arena bytes the site's records take (a multiple of 2K, the
- * lane's share), or -1 (nothing written) when a contributing read has
- * minq >= 64: the 8-bit record cannot hold its q, and the site goes to the
- * deep kernel. */
-template <int K>
-__device__ __forceinline__ int sort_site_wide(const uint32_t (&rd)[32], const WideSite &w, uint32_t ref16,
-                                               uint32_t cap, uint8_t *arena, uint32_t base, Slot3 *st2)
-{
-    const uint32_t lane = lane_id();
-    const uint32_t nt = w.nt, nn = w.nn;
-    uint32_t tb, th;
-    nt_tables(ref16, tb, th);
-    uint32_t v[1][K];
-    uint32_t a_t = 0, a_n = 0;
-    GroupCount<K> gc;
-    gc.zero();
-    /* registers whose elements are all pads (rd = 0: key 0xffff, no rms or
-     * count) skip the key build: a wave-uniform bound on the live elements */
-    const uint32_t live = w.split ? 2u * max(nt, nn) : wide_unit_slots(w);
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-        if ((uint32_t)r * 128u >= live) {
-            v[0][r] = 0xffffffffu;
-            continue;
-        }
-        const uint32_t e0 = ((uint32_t)r * 64u + lane) * 2u;
-        const bool tum = w.split ? lane < 32u : e0 < w.sp;
-        const uint32_t rd0 = rd[2 * r], rd1 = rd[2 * r + 1];
-        const uint32_t sb = tum ? 0u : 0x8000u;
-#ifndef SS_AB_WNOKEY
-        const uint32_t k0 = read_key16(rd0, tb, th, sb), k1 = read_key16(rd1, tb, th, sb);
-#else
-        const uint32_t k0 = (rd0 & 0x7fffu) | sb, k1 = (rd1 & 0x7fffu) | sb;
-#endif
-        const uint32_t t0 = min(rd0 & 0x7fu, cap), t1 = min(rd1 & 0x7fu, cap);
-        const uint32_t x = t0 * t0 + t1 * t1;
-        a_t += tum ? x : 0u;
-        a_n += tum ? 0u : x;
-        gc.add(k0, k1, tum);
-        v[0][r] = k0 | k1 << 16;
-    }
-    if (__ballot(!wide_q_fits<K>(v))) return -1;
-    /* group sizes before the sort (see GroupCount) */
-    uint32_t wt[2], wn[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        wt[i] = wave_sum(gc.t[i]);
-        wn[i] = wave_sum(gc.n[i]);
-    }
-    if (SS_PRIO_WIDE) __builtin_amdgcn_s_setprio(SS_PRIO_WIDE);
-#ifndef SS_AB_WNOSORT
-    packed_bitonic_flip<1, K>(v, !w.split);
-#endif
-    if (SS_PRIO_WIDE) __builtin_amdgcn_s_setprio(0);
-    const uint32_t c1 = GroupCount<K>::field(wt, 0), c2 = c1 + GroupCount<K>::field(wt, 1);
-    const uint32_t c3 = c2 + GroupCount<K>::field(wt, 2), c4 = c3 + GroupCount<K>::field(wt, 3);
-    const uint32_t c5 = c4 + GroupCount<K>::field(wn, 0), c6 = c5 + GroupCount<K>::field(wn, 1);
-    const uint32_t c7 = c6 + GroupCount<K>::field(wn, 2), c8 = c7 + GroupCount<K>::field(wn, 3);
-    /* The record of network element e goes to base + e: the lane's 2K
-     * elements are contiguous, so they leave as 16-byte stores.  The tumor
-     * groups start at base, the normal ones at base + nb; pad and q = 0
-     * elements land past each sample's groups and are never read.  Lanes
-     * wholly past the extent store nothing (the next site starts there). */
-    const uint32_t nb = w.split ? 64u * K : c4;
-#ifdef SS_AB_WNOREC
-    if (lane == 0 && w.unit != 2u) { st2[0].rec_n = base | nt << 16; st2[0].cnt01 = c1; st2[0].cnt23 = c3; st2[0].rms = wave_sum(a_t); }
-    if (lane == 0 && w.unit != 1u) { st2[1].rec_n = (base + nb) | nn << 16; st2[1].cnt01 = c5; st2[1].cnt23 = c7; st2[1].rms = v[0][0]; }
-    return (int)(((w.split ? nb + (c8 - c4) : c8) + 31u) & ~31u);
-#endif
-    /* extents stay multiples of 16 bytes: every unit's stores are 16-byte aligned */
-    constexpr uint32_t XR = K < 8 ? 16u : 2u * K;
-    const uint32_t extent = ((w.split ? nb + (c8 - c4) : c8) + XR - 1u) & ~(XR - 1u);
-    if constexpr (K == 4) {
-        if (lane * 8u < extent) {
-            uint32_t d[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const uint32_t x = v[0][2 * j], y = v[0][2 * j + 1];
-                d[j] = key_to_rec8(x & 0xffffu) | key_to_rec8(x >> 16) << 8 |
-                       key_to_rec8(y & 0xffffu) << 16 | key_to_rec8(y >> 16) << 24;
-            }
-            *reinterpret_cast<uint2 *>(arena + base + lane * 8u) = make_uint2(d[0], d[1]);
-        }
-    } else if (lane * (2u * K) < extent) {
-#pragma unroll
-        for (int q = 0; q < K / 8; ++q) {
-            uint32_t d[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t x = v[0][8 * q + 2 * j], y = v[0][8 * q + 2 * j + 1];
-                d[j] = key_to_rec8(x & 0xffffu) | key_to_rec8(x >> 16) << 8 |
-                       key_to_rec8(y & 0xffffu) << 16 | key_to_rec8(y >> 16) << 24;
-            }
-            *reinterpret_cast<uint4 *>(arena + base + lane * (2u * K) + 16u * (uint32_t)q) =
-                make_uint4(d[0], d[1], d[2], d[3]);
-        }
-    }
-    const uint32_t rms_t = wave_sum(a_t), rms_n = wave_sum(a_n);
-    /* a sample unit fills only its sample's slot */
-    if (lane == 0 && w.unit != 2u) {
-        st2[0].rec_n = base | nt << 16;
-        st2[0].cnt01 = c1 | (c2 - c1) << 16;
-        st2[0].cnt23 = (c3 - c2) | (c4 - c3) << 16;
-        st2[0].rms = rms_t;
-    }
-    if (lane == 0 && w.unit != 1u) {
-        st2[1].rec_n = (base + nb) | nn << 16;
-        st2[1].cnt01 = (c5 - c4) | (c6 - c5) << 16;
-        st2[1].cnt23 = (c7 - c6) | (c8 - c7) << 16;
-        st2[1].rms = rms_n;
-    }
-    return (int)extent;
-}
-
-}  // namespace
-
-__global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
-{
-    __shared__ double fk[256];
-    __shared__ WideLds L;
-    const unsigned long long acc = *a.deep_acc;
-    const uint32_t nsegs = min((uint32_t)(acc >> 32), a.deep_nseg), total = (uint32_t)acc;
-    if (nsegs == 0u) return;                 /* the main kernel listed no site (every workgroup) */
-    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
-    __syncthreads();
-    const uint32_t lane = lane_id();
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   /* wave-uniform */
-    uint8_t *arena = L.arena[wv];
-    Slot3 *slot = L.slot[wv];
-    SlotRes *res = L.res[wv];
-    uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
-    const uint32_t cap = (uint32_t)a.m.cap_mapQ;
-    const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
-    /* the listed entries (segments back to back in listing order), GB at a
-     * time, handed out by an atomic counter: waves that draw dense sites do
-     * fewer chunks */
-    for (;;) {
-        uint32_t ch = 0;
-        if (lane == 0u) ch = atomicAdd(a.wide_next, 1u);
-        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * GB;
-        if (first >= total) break;
-        const uint32_t nlist = total - first < GB ? total - first : GB;
-        /* the segment holding entry `first` (binary search over the ascending
-         * offsets, wave-uniform), then lane k steps to entry first + k's */
-        const ss_score_args &k = kernarg_args();
-        uint32_t lo = 0, hi = nsegs;
-        while (hi - lo > 1u) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (k.deep_off[mid] <= first) lo = mid;
-            else hi = mid;
-        }
-        uint32_t i = 0, s_cur = 0;
-        WideSite w_cur = {0, 0, 0, 0, 0, 0, 0, false, false};
-        /* the chunk's descriptors, lane k = entry k, loaded at once (one
-         * exposed chain of dependent loads per chunk, not per site) */
-        uint32_t c_s = 0, c_ot = 0, c_ot1 = 0, c_on = 0, c_on1 = 0, c_ref = 0;
-        if (lane < nlist) {
-            const uint32_t p = first + lane;
-            uint32_t sg = lo;
-            while (sg + 1u < nsegs && k.deep_off[sg + 1u] <= p) ++sg;
-            c_s = k.deep_list[(size_t)k.deep_segs[sg] * k.deep_seg_cap + (p - k.deep_off[sg])];
-            c_ot = k.off_t[c_s];
-            c_ot1 = k.off_t[c_s + 1];
-            c_on = k.off_n[c_s];
-            c_on1 = k.off_n[c_s + 1];
-            const uint32_t rc = k.ref[c_s];
-            c_ref = rc | (uint32_t)ss_tab_nt16(k.m)[rc] << 8;
-        }
-        auto describe = [&](uint32_t k, uint32_t &s, WideSite &w) {
-            s = rl(c_s, k);
-            w.ot = rl(c_ot, k);
-            w.nt = rl(c_ot1, k) - w.ot;
-            w.on = rl(c_on, k);
-            w.nn = rl(c_on1, k) - w.on;
-            w.ref = rl(c_ref, k);
-            wide_place(w, end_t, end_n);
-        };
-        if (nlist) describe(0, s_cur, w_cur);
-        uint32_t ext_t = 0;             /* arena bytes of the current site's tumor unit */
-        bool dead = false;              /* that tumor unit sent the site to the deep list */
-        while (i < nlist) {
-            int G = 0;
-            uint32_t used = 0;
-            while (i < nlist) {
-                const uint32_t s = s_cur;
-                const WideSite w = w_cur;
-                const uint32_t slots = wide_unit_slots(w);
-                /* the most arena the site can take (sort_site_wide's extents), checked where a site starts */
-                const uint32_t kb = slots <= 1024u ? 16u : 32u;
-                const uint32_t bound = w.unit ? ((w.nt + 31u) & ~31u) + ((w.nn + 31u) & ~31u)
-                                              : ((w.split ? 32u * kb + w.nn : slots) + kb - 1u) & ~(kb - 1u);
-                if (w.unit != 2u && used + bound > WIDE_ARENA && !w.over) break;   /* next sub-group */
-                /* the unit's reads, loaded where it is sorted (the other waves
-                 * of the SIMD hide the latency) */
-                uint32_t cur[32];
-                wide_load(kernarg_args(), w, cur);
-                if (w.unit == 1u) {                       /* next: the same site's normal */
-                    w_cur = wide_normal_unit(w);
-                } else {
-                    if (i + 1 < nlist) describe(i + 1, s_cur, w_cur);
-                    ++i;
-                }
-                if (w.unit == 2u && dead) {               /* already on the deep list */
-                    dead = false;
-                    continue;
-                }
-                const uint32_t ref16 = w.ref >> 8;
-                const uint32_t base = used + (w.unit == 2u ? ext_t : 0u);
-                const int ext = w.over ? -1
-                              : w.unit && slots <= 512u ? sort_site_wide<4>(cur, w, ref16, cap, arena, base, slot + 2 * G)
-                              : slots <= 1024u ? sort_site_wide<8>(cur, w, ref16, cap, arena, base, slot + 2 * G)
-                                               : sort_site_wide<16>(cur, w, ref16, cap, arena, base, slot + 2 * G);
-                if (ext < 0) {
-                    if (lane == 0) {
-                        const ss_score_args &k = kernarg_args();
-                        const uint32_t d = atomicAdd(k.deep2_count, 1u);
-                        if (d < k.deep_cap) k.deep2_list[d] = s;
-                        else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
-                    }
-                    dead = w.unit == 1u;
-                    continue;
-                }
-                if (w.unit == 1u) {                       /* the site completes with its normal unit */
-                    ext_t = (uint32_t)ext;
-                    continue;
-                }
-                if (lane == 0) {
-                    sites[G] = s;
-                    refcs[G] = w.ref;
-                }
-                used += (w.unit == 2u ? ext_t : 0u) + (uint32_t)ext;
-                ++G;
-            }
-            wave_sync();
-            if (G) finish_sub<uint8_t>(kernarg_args(), G, arena, slot, res, sites, refcs, fk);
-        }
-    }
-}
 
 /* --------------------------------------------------------------------------
  * Group kernel: the wide list's sites with at most SS_WIDE_MAXSLOTS reads per
  * sample, sorted by lane groups (round 3; replaces the wave-per-site network
- * of ss_score_wide on the launch path).
+ * of round 2's ss_score_wide).
  *
  * A sort unit is one (site, sample) of n reads; it takes U = 1, 2, 4, 8 or 16
  * lanes (128 reads each).  Every lane builds and sorts its 128 keys exactly as
@@ -1993,17 +1346,18 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_wide(ss_score_args a)
  * ------------------------------------------------------------------------ */
 namespace {
 
+#define GP_WAVES (SS_WIDE_BLOCK / 64)         /* 8 waves, one workgroup per CU (LDS) */
 #define GP_ARENA 16384                     /* record bytes per wave (16 sites of ~1000 reads) */
 #define GP_UNITS (2 * GB)
 
 struct alignas(16) GroupLds {
-    uint8_t  arena[WIDE_WAVES][GP_ARENA];
-    Slot3    slot[WIDE_WAVES][2 * GB];
-    SlotRes  res[WIDE_WAVES][2 * GB];
-    uint32_t site[WIDE_WAVES][GB];
-    uint32_t refc[WIDE_WAVES][GB];
-    uint32_t ucnt[WIDE_WAVES][GP_UNITS][4];          /* per unit: counts of bases 0, 2 | 1, 3 (16-bit), rms, wild */
-    uint8_t  unit_of[WIDE_WAVES][GP_UNITS * 16];     /* lane position -> unit */
+    uint8_t  arena[GP_WAVES][GP_ARENA];
+    Slot3    slot[GP_WAVES][2 * GB];
+    SlotRes  res[GP_WAVES][2 * GB];
+    uint32_t site[GP_WAVES][GB];
+    uint32_t refc[GP_WAVES][GB];
+    uint32_t ucnt[GP_WAVES][GP_UNITS][4];          /* per unit: counts of bases 0, 2 | 1, 3 (16-bit), rms, wild */
+    uint8_t  unit_of[GP_WAVES][GP_UNITS * 16];     /* lane position -> unit */
 };
 
 /* cross-lane compare-exchange: the lower lane keeps (min lo, max hi) */
@@ -2083,7 +1437,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
         const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * GB;
         if (first >= total) break;
         const uint32_t nlist = total - first < GB ? total - first : GB;
-        /* the chunk's sites, lane k = entry k (as in ss_score_wide) */
+        /* the chunk's sites, lane k = entry k */
         const ss_score_args &k = kernarg_args();
         uint32_t lo = 0, hi = nsegs;
         while (hi - lo > 1u) {
@@ -2174,6 +1528,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
                 in.na4 = (in.na + 3u) & ~3u;
                 in.nb = 0u;
                 in.nca = in.na4 >> 2;
+                asm("" : "+v"(in.nca));         /* as in ss_score_main */
                 in.nab = in.na4;
                 const uint32_t *base_s = smp ? a.reads_n : a.reads_t;
                 const uint32_t start = act ? rofs + 128u * j : 0u;
@@ -2253,7 +1608,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
  *
  * No sort: the fold only needs each (sample, base) group's reads in the
  * reference's descending key order (sniper_maqcns.c:157-172), and reads with
- * equal (q, strand) contribute identical terms (see read_key16), so a
+ * equal (q, strand) contribute identical terms (see the order key), so a
  * counting sort over the order-relevant key fields is exact.  Bins of one
  * base group, ascending in key order (DBIN per group):
  *   minq <  4:  minq<<5 | hasbase<<4 | strand<<3 | E<<1 | nz        0..127
@@ -2503,7 +1858,7 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
             if (a.glf) store_glf(&a.glf[2ull * s + smp], ref16, lk, min_lk, rms_q, r.depth);
         }
         wave_sync();
-        if (lane == 0u) decide_site(a, s, refc | ref16 << 8, D.res[0], D.res[1]);
+        if (lane == 0u) decide_site(a, ss_tab_qadd(a.m), s, refc | ref16 << 8, D.res[0], D.res[1]);
         wave_sync();
     }
 }
@@ -2555,11 +1910,7 @@ int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int de
     hipLaunchKernelGGL(ss_score_main, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[1], s);
-#ifndef SS_AB_OLDWIDE
     hipLaunchKernelGGL(ss_score_group, dim3(wide_grid), dim3(SS_WIDE_BLOCK), 0, s, a);
-#else
-    hipLaunchKernelGGL(ss_score_wide, dim3(wide_grid), dim3(SS_WIDE_BLOCK), 0, s, a);
-#endif
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[2], s);
     hipLaunchKernelGGL(ss_score_deep, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);

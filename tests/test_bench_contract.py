@@ -16,15 +16,16 @@ GRCH38 = [248956422, 242193529, 198295559, 190214555, 181538259, 170805979, 1593
 @pytest.mark.gpu
 def test_bench_json_contract():
     """Default workload (C4, contig-sharded GRCh38, here / 4096): the driver's
-    fields, strong scaling, the roofline of the timed launches, the weak line
-    and the 1-core reference baseline with its parity spot check."""
+    fields, strong scaling (a fixed --c4-scale), the roofline of the timed
+    launches, the strong-scaling line and the 1-core reference baseline with
+    its parity spot check."""
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--c4-scale", "4096", "--steps", "2",
-                        "--warmup", "1", "--cpu-sample", "20000", "--weak-sites", "262144", "--weak-steps", "2"],
+                        "--warmup", "1", "--cpu-sample", "20000", "--strong-scale", "8192", "--strong-steps", "2"],
                        capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
-              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "weak_scaling"):
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "strong_scaling"):
         assert k in r, k
     assert r["n_gpus"] == 1 and r["steps"] == 2 and r["value"] > 1e8 and r["higher_is_better"] is True
     assert r["scaling"] == "strong" and r["unit"] == "sites/s" and r["config"]["workload"].startswith("C4")
@@ -44,7 +45,10 @@ def test_bench_json_contract():
         assert v["insts_per_site"] > 50 and 0 < v["issue_frac_lower_bound"] < 1.0, v
     cb = r["cpu_baseline"]
     assert cb["cores"] == 1 and cb["value"] > 0 and cb["parity_vs_gpu"] is True
-    assert r["weak_scaling"]["scaling"] == "weak" and r["weak_scaling"]["value"] > 1e8
+    st = r["strong_scaling"]
+    assert st["scaling"] == "strong" and st["value"] > 1e8 and st["c4_scale"] == 8192
+    assert st["genome_sites_per_step"] == sum(-(-length // 8192) for length in GRCH38)
+    assert r["config"]["planned_hbm_bytes_per_rank"] >= r["ranks"][0]["hbm_peak_allocated_bytes"] * 0.5
 
 
 @pytest.mark.gpu
@@ -122,8 +126,8 @@ def test_bench_c4_ranks_self_spawned_gloo(gpus):
     max rank time is the value."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo",
-                        "--c4-scale", "8192", "--steps", "2", "--warmup", "1", "--weak-sites", "65536",
-                        "--weak-steps", "2"], env=env, capture_output=True, text=True, timeout=600)
+                        "--c4-scale", "8192", "--steps", "2", "--warmup", "1", "--strong-scale", "16384",
+                        "--strong-steps", "2"], env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["n_gpus"] == gpus and len(r["ranks"]) == gpus and r["scaling"] == "strong"
@@ -132,7 +136,7 @@ def test_bench_c4_ranks_self_spawned_gloo(gpus):
     assert sorted(contigs) == sorted(n for n, _ in GRCH38_NAMES) and len(set(contigs)) == 24
     genome = r["config"]["genome_sites_per_step"]
     assert sum(x["sites_per_step"] for x in r["ranks"]) == genome
-    assert r["value"] > 0 and "cpu_baseline" not in r and r["weak_scaling"]["value"] > 0
+    assert r["value"] > 0 and "cpu_baseline" not in r and r["strong_scaling"]["value"] > 0
     worst = max(x["ms_per_step"] for x in r["ranks"])
     assert abs(r["ms_per_step"] - worst) < 1e-3 + 1e-6 * worst
     assert abs(r["value"] - genome * 2 / (worst * 2 * 1e-3)) / r["value"] < 1e-3
@@ -184,3 +188,23 @@ def test_c4_layout_partitions_the_genome():
     import importlib
     sh = importlib.import_module("somatic_sniper_amd.sharding")
     assert sh.plan_imbalance(GRCH38, sh.shard_contigs(GRCH38, 8, restarts=0)) < 1.04
+
+
+def test_c4_default_sizing_fits_hbm():
+    """CPU: --c4-scale auto gives every GPU one eighth of GRCh38 (8 / N), so
+    N = 8 is the whole 3.09e9-site genome of BASELINE configs[3]; the planned
+    resident bytes per rank (reads, offsets, ref, scores, the largest launch's
+    working set) fit 85% of one MI355X's 288 GB at every N, and the per-GPU
+    share stays within 1% of the 8-GPU one."""
+    b = _bench()
+    hbm = 288e9
+    assert [b.c4_auto_scale(w) for w in (1, 2, 4, 8, 16)] == [8, 4, 2, 1, 1]
+    per8 = max(b.c4_rank_bytes(1, 8, 60.0, 30.0, 1 << 26))
+    assert 1.3e11 < per8 < 0.85 * hbm, per8            # about 143 GB per GPU
+    _, sizes, plan = b.c4_layout(1, 8)
+    assert sum(sizes) == sum(GRCH38)
+    for world in (1, 2, 4):
+        per = max(b.c4_rank_bytes(b.c4_auto_scale(world), world, 60.0, 30.0, 1 << 26))
+        assert per < 0.85 * hbm and abs(per / per8 - 1) < 0.01, (world, per, per8)
+    # a site's bytes bound the generator's mean non-deleted depth (0.99 (lt + ln))
+    assert b.site_bytes(60, 30) >= 4 * 89.1 + 13

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Out-of-tree timing ablations of the main kernel (never shipped).
+
+Writes a copy of somatic-sniper_amd/csrc/ss_kernels.hip with the named phases
+of ss_score_main replaced by cheap stand-ins, for `make variant` and
+tools/ab.sh; the scores of such a build are meaningless (ab.sh with
+AB_NOPARITY=1).  The shipped source carries no switches for this.
+
+  python tools/ablate.py OUT.hip nonet norec nofold nofin nodecide
+  make -C somatic-sniper_amd variant V=abl KSRC=build/exp_abl.hip
+
+Phases (round 3's SS_AB_* switches):
+  nonet     no bitonic network (keys stay unsorted)
+  norec     no fold records written to LDS
+  nofold    no ordered fold (es / fs from the group counts)
+  nofin     no likelihoods / glf2cns (fields from the fold sums)
+  nodecide  no site decision (score = tumor cns word)
+and of ss_score_group (the C5 path):
+  gnosort   no in-lane network (ln_levels)
+  gnomerge  no cross-lane merge levels (gp_level)
+  gnorec    no fold records written to the arena
+  gnofold   no ordered fold in finish_sub (sums from the counts)
+  gnofin    no likelihoods in finish_sub (p from the sums)
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "somatic-sniper_amd", "csrc", "ss_kernels.hip")
+
+EDITS = {
+    "nonet": [("            ln_levels<LN_R, 2>(v);\n            ln_records(", "            ln_records(")],
+    "norec": [("            ln_records(v, 4u * nch, L, lane);\n", "")],
+    "nofold": [("                ln_fold(L, lane, k ? tot_a : 0u, k ? acc.cnt_b : acc.cnt_a, fk, es, fs, c);\n",
+                "                for (int b = 0; b < 4; ++b) { es[b] = fs[b] = (float)(acc.cnt_a >> b); "
+                "c[b] = (acc.cnt_a >> (8 * b)) & 0xffu; }\n")],
+    "nofin": [("                ln_finish(es, fs, c, smpN ? nn : nt, k ? acc.rms_b : acc.rms_a, a.m, l03, l47, l89, cn, mq);\n",
+               "                l03 = __float_as_uint(es[0]); l47 = __float_as_uint(fs[1]); l89 = c[2]; "
+               "cn = 0x11000000u; mq = c[3];\n")],
+    "nodecide": [("        if (ok) decide_site(kernarg_args(), qtab, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);\n",
+                  "        if (ok) a.score[s] = (int)L.res[lane][0].cns;\n")],
+    "gnosort": [("                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);\n                ln_levels<LN_R, 2>(v);\n",
+                 "                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);\n")],
+    "gnomerge": [("                if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }\n"
+                  "                if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }\n"
+                  "                if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }\n"
+                  "                if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }\n", "")],
+    "gnorec": [("                    if (4 * i < lim) *reinterpret_cast<uint32_t *>(arena + ubase + 4u * (uint32_t)i) = "
+                "ln_rec_dword(v, i);\n", "")],
+    "gnofold": [("        fold_sample<RecT>(rec, cnt, fk, role, acc);\n",
+                 "        for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b] + (float)rec[b];\n")],
+    "gnofin": [("    geno_p5(role, es, fs, c, tot, a.m, mine);\n",
+                "    for (int t = 0; t < 5; ++t) mine[t] = es[t & 3] + (float)c[t & 3];\n")],
+}
+
+
+def main():
+    if len(sys.argv) < 3:
+        sys.exit(__doc__)
+    out, phases = sys.argv[1], sys.argv[2:]
+    s = open(SRC).read()
+    for ph in phases:
+        if ph not in EDITS:
+            sys.exit(f"unknown phase {ph}; known: {', '.join(EDITS)}")
+        for old, new in EDITS[ph]:
+            if s.count(old) != 1:
+                sys.exit(f"{ph}: the kernel source no longer has exactly one {old.strip()[:60]!r}")
+            s = s.replace(old, new)
+    open(out, "w").write(s)
+
+
+if __name__ == "__main__":
+    main()
