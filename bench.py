@@ -609,6 +609,7 @@ def main():
             pre = score[k][:sample].cpu().numpy()
     reads_all = float(np.sum(reads))
     sites_all = sum(d["n_sites"] for d in batches)
+    n_batches = len(batches)
     # free the resident batches before the next line / the counter passes
     del batches, score
     torch.cuda.synchronize(dev)
@@ -676,7 +677,7 @@ def main():
         assert sum(r["sites_per_step"] for r in ranks) == genome_sites, "a contig scored twice or not at all"
     else:
         config = {"workload": f"synthetic shard per GPU, {args.lt:g}xT/{args.ln:g}xN Poisson depth",
-                  "sites_per_step_per_gpu": args.sites, "resident_batches": len(batches)}
+                  "sites_per_step_per_gpu": args.sites, "resident_batches": n_batches}
     config.update({"mean_reads_per_site": round(mean_reads, 2),
                    "parallelism": f"{'contig' if c4 else 'region'}-sharded x{world}, no collectives",
                    "model_tables_pinned": pinned, "library": library_id(pkg)})
