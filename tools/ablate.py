@@ -15,6 +15,7 @@ Phases (round 3's SS_AB_* switches):
   nofold    no ordered fold (es / fs from the group counts)
   nofin     no likelihoods / glf2cns (fields from the fold sums)
   nodecide  no site decision (score = tumor cns word)
+  nominor   only the largest base group's chain per sample (the other three skipped)
 and of ss_score_group (the C5 path):
   gnosort   no in-lane network (ln_levels)
   gnomerge  no cross-lane merge levels (gp_level)
@@ -39,6 +40,8 @@ EDITS = {
                "cn = 0x11000000u; mq = c[3];\n")],
     "nodecide": [("        if (ok) decide_site(kernarg_args(), qtab, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);\n",
                   "        if (ok) a.score[s] = (int)L.res[lane][0].cns;\n")],
+    "nominor": [("        ln_chain(L, lane, st[b], isbig ? 0u : c[b], fk, eb, fb);\n",
+                 "        eb = fb = 0.0f;\n")],
     "gnosort": [("                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);\n                ln_levels<LN_R, 2>(v);\n",
                  "                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);\n")],
     "gnomerge": [("                if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }\n"

@@ -4,7 +4,7 @@
 OUT=$1; shift
 for i in $(seq 1 30); do
   /usr/local/graft/bin/gpurun "$@" > "$OUT" 2>&1
-  if grep -q "nothing was charged\|stopped responding while being prepared\|backing off" "$OUT"; then
+  if grep -q "nothing was charged\|stopped responding while being prepared\|backing off\|was taken away by the GPU service\|has no free box right now" "$OUT"; then
     sleep 90; continue
   fi
   break
