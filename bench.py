@@ -722,7 +722,13 @@ def main():
             rd, wr = 2.0 * pc["FETCH_SIZE"] * 1024.0, pc["WRITE_SIZE"] * 1024.0
             rf = result["roofline"]
             rf["traffic"] = rd + wr
-            rf["traffic_over_algorithmic"] = round((rd + wr) / alg_bytes, 4)
+            # the counter child scores the first --pmc-batches launches (full
+            # 2^26-site launches at C4): compare with their own algorithmic bytes
+            alg_pmc = float(np.mean(bytes_of[:args.pmc_batches])) if c4 else alg_bytes
+            rf["traffic_over_algorithmic"] = round((rd + wr) / alg_pmc, 4)
+            rf["traffic_bytes_per_site"] = {"read": round(rd / pc["_sites_per_launch"], 2),
+                                            "write": round(wr / pc["_sites_per_launch"], 2),
+                                            "algorithmic": round(alg_pmc / pc["_sites_per_launch"], 2)}
             cyc = pc["GRBM_GUI_ACTIVE"] / 8.0                       # kernel cycles
             simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
             site_n = pc["_sites_per_launch"]

@@ -253,7 +253,8 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     if (o->calls && !o->n_calls) return SS_E_INVAL;
     HIPCHK(hipSetDevice(c->device));
     /* main kernel: 4 waves per workgroup, one 64-site block per wave per
-     * iteration (lane = site), grid-strided; 4 workgroups fit a CU (LDS).
+     * iteration (lane = site), grid-strided; 3 workgroups are resident per CU
+     * (166 VGPRs -> 3 waves per SIMD; 52.5 KB of LDS each).
      * Each wave owns a deep-list segment as long as the most blocks it can
      * visit, times 64 sites. */
     const uint64_t site_blocks = (b->n_sites + SS_MAIN_SITES - 1) / SS_MAIN_SITES;

@@ -83,7 +83,8 @@ struct ss_score_args {
 /* Launch geometry constants shared with the host. */
 #define SS_MAIN_BLOCK      256   /* 4 waves, each 64 sites at a time (lane = site) */
 #define SS_MAIN_SITES      64    /* sites per main-kernel wave block           */
-#define SS_MAIN_GRID_PER_CU 128  /* main-kernel workgroups per CU: 4 resident, 32 rounds of short-lived waves (+5.5% over 16) */
+#define SS_MAIN_GRID_PER_CU 128  /* main-kernel workgroups per CU: 3 resident (166 VGPRs, 52.5 KB LDS each),
+                                    the rest queued as short-lived waves (+5.5% over 16 per CU) */
 #define SS_DEEP_BLOCK      256
 #ifndef SS_WIDE_BLOCK
 #define SS_WIDE_BLOCK      512   /* 8 waves, one workgroup per CU (LDS); 12 waves with a

@@ -1433,7 +1433,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
     for (;;) {
         uint32_t ch = 0;
-        if (lane == 0u) ch = atomicAdd(a.wide_next, 1u);
+        if (lane == 0u) ch = atomicAdd(kernarg_args().wide_next, 1u);
         const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * GB;
         if (first >= total) break;
         const uint32_t nlist = total - first < GB ? total - first : GB;
@@ -1530,7 +1530,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
                 in.nca = in.na4 >> 2;
                 asm("" : "+v"(in.nca));         /* as in ss_score_main */
                 in.nab = in.na4;
-                const uint32_t *base_s = smp ? a.reads_n : a.reads_t;
+                const uint32_t *base_s = smp ? kernarg_args().reads_n : kernarg_args().reads_t;
                 const uint32_t start = act ? rofs + 128u * j : 0u;
                 in.pa = base_s + start;
                 in.pb = in.pa;
@@ -1776,18 +1776,21 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
     const uint32_t lane = lane_id();
     const uint32_t grp = ((lane >> 3) & 1u) * 4u + ((lane >> 1) & 3u);  /* fold lanes 0..15: sample, base */
     for (uint32_t w = blockIdx.x * DEEP_WAVES + wv; w < lim; w += gridDim.x * DEEP_WAVES) {
-        const uint32_t s = a.deep2_list[w];
-        const uint32_t ot = a.off_t[s], ot1 = a.off_t[s + 1], on = a.off_n[s], on1 = a.off_n[s + 1];
+        /* arguments re-read from the kernarg segment where used: they do not
+         * stay live in SGPRs across the site loop (44 SGPR spills before) */
+        const ss_score_args &k = kernarg_args();
+        const uint32_t s = k.deep2_list[w];
+        const uint32_t ot = k.off_t[s], ot1 = k.off_t[s + 1], on = k.off_n[s], on1 = k.off_n[s + 1];
         if (!site_wellformed(ot, ot1, end_t) || !site_wellformed(on, on1, end_n)) {
             if (lane == 0) {
-                atomicOr(a.err, SS_KERR_MALFORMED);
-                a.score[s] = -2;
+                atomicOr(k.err, SS_KERR_MALFORMED);
+                k.score[s] = -2;
             }
             continue;                                  /* wave-uniform */
         }
         const uint32_t nt = ot1 - ot, nn = on1 - on;
-        const uint32_t refc = a.ref[s];
-        const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
+        const uint32_t refc = k.ref[s];
+        const uint32_t ref16 = ss_tab_nt16(k.m)[refc];
         uint32_t tb, th;
         nt_tables(ref16, tb, th);
         if (lane < 2u) D.rms[lane] = 0ull;
@@ -1796,8 +1799,8 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
         /* the first pass also counts the bottom window: when every bin is in
          * it (minq <= 60 everywhere) it is the only pass */
         uint64_t rt = 0, rn = 0;
-        uint32_t top = max(deep_pass<0>(a.reads_t + ot, nt, tb, th, cap, 0, DW_BINS, D.hist, rt),
-                           deep_pass<0>(a.reads_n + on, nn, tb, th, cap, 0, DW_BINS, D.hist + 4 * DW_BINS, rn));
+        uint32_t top = max(deep_pass<0>(k.reads_t + ot, nt, tb, th, cap, 0, DW_BINS, D.hist, rt),
+                           deep_pass<0>(k.reads_n + on, nn, tb, th, cap, 0, DW_BINS, D.hist + 4 * DW_BINS, rn));
         top = wave_max(top);
         atomicAdd(&D.rms[0], (unsigned long long)rt);
         atomicAdd(&D.rms[1], (unsigned long long)rn);
@@ -1811,8 +1814,8 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
                 deep_zero(D.hist);
                 wave_sync();
                 uint64_t unused = 0;
-                deep_pass<1>(a.reads_t + ot, nt, tb, th, cap, lo, hi, D.hist, unused);
-                deep_pass<1>(a.reads_n + on, nn, tb, th, cap, lo, hi, D.hist + 4 * DW_BINS, unused);
+                deep_pass<1>(k.reads_t + ot, nt, tb, th, cap, lo, hi, D.hist, unused);
+                deep_pass<1>(k.reads_n + on, nn, tb, th, cap, lo, hi, D.hist + 4 * DW_BINS, unused);
             }
             counted = false;
             wave_sync();
@@ -1846,7 +1849,7 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
         const uint32_t n = smp ? nn : nt;
         const uint64_t rms = D.rms[smp];
         uint32_t lk[10], min_lk, rms_q, cns;
-        glf_and_cns((int)(lane & 3u), es, fs, c, n, rms, a.m, lk, min_lk, rms_q, cns);
+        glf_and_cns((int)(lane & 3u), es, fs, c, n, rms, k.m, lk, min_lk, rms_q, cns);
         if (lane == 0u || lane == 4u) {
             SlotRes &r = D.res[smp];
 #pragma unroll
@@ -1855,10 +1858,10 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
             r.depth = n > 16777215u ? 16777215u : n;
             r.min_lk = (uint8_t)min_lk;
             r.rms_q = (uint8_t)rms_q;
-            if (a.glf) store_glf(&a.glf[2ull * s + smp], ref16, lk, min_lk, rms_q, r.depth);
+            if (k.glf) store_glf(&k.glf[2ull * s + smp], ref16, lk, min_lk, rms_q, r.depth);
         }
         wave_sync();
-        if (lane == 0u) decide_site(a, ss_tab_qadd(a.m), s, refc | ref16 << 8, D.res[0], D.res[1]);
+        if (lane == 0u) decide_site(k, ss_tab_qadd(k.m), s, refc | ref16 << 8, D.res[0], D.res[1]);
         wave_sync();
     }
 }
