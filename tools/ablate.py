@@ -16,6 +16,7 @@ Phases (round 3's SS_AB_* switches):
   nofin     no likelihoods / glf2cns (fields from the fold sums)
   nodecide  no site decision (score = tumor cns word)
   nominor   only the largest base group's chain per sample (the other three skipped)
+  noload    reads synthesised in registers instead of loaded (key build without memory)
 and of ss_score_group (the C5 path):
   gnosort   no in-lane network (ln_levels)
   gnomerge  no cross-lane merge levels (gp_level)
@@ -42,6 +43,10 @@ EDITS = {
                   "        if (ok) a.score[s] = (int)L.res[lane][0].cns;\n")],
     "nominor": [("        ln_chain(L, lane, st[b], isbig ? 0u : c[b], fk, eb, fb);\n",
                  "        eb = fb = 0.0f;\n")],
+    "noload": [("    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */\n",
+                "    if (true) {\n#pragma unroll\n        for (int t = 0; t < 4; ++t) "
+                "x[t] = ((in.na + 4u * c + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;\n        return;\n    }\n"
+                "    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */\n")],
     "gnosort": [("                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);\n                ln_levels<LN_R, 2>(v);\n",
                  "                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);\n")],
     "gnomerge": [("                if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }\n"
