@@ -41,7 +41,7 @@ struct ss_ctx {
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
     uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6..7] listed
-                                 entries | segments << 32, [8] the wide kernel's chunk counter */
+                                 entries | segments << 32, [8] the group kernel's chunk counter */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
     uint32_t *d_deep_seg;     /* listed segments' first entries, then their main-wave ids */
@@ -228,7 +228,7 @@ extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double
 }
 
 /* the deep list buffer holds two lists of deep_cap entries: the main
- * kernel's per-wave segments (deep) and the wide kernel's overflow (deep2).
+ * kernel's per-wave segments (deep) and the group kernel's overflow (deep2).
  * Grown on the launch stream `s`, which has already waited for the
  * context's previous launch (the last user of the old list). */
 static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
@@ -269,7 +269,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     if (c->launched && s != c->last_stream) HIPCHK(hipStreamWaitEvent(s, c->done, 0));
     int rc = ensure_deep_cap(c, nseg * seg_cap, s);
     if (rc) return rc;
-    /* counters: deep2, listed segments and entries, the wide kernel's next
+    /* counters: deep2, listed segments and entries, the group kernel's next
      * chunk (err is sticky until ss_ctx_check) */
     HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 4 * sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));

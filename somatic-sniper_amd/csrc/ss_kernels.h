@@ -67,11 +67,11 @@ struct ss_score_args {
     uint32_t  *deep_segs;     /* [deep_nseg] ids of the main waves that listed sites, compacted */
     uint32_t  *deep_off;      /* [deep_nseg] their first entry in the listed order (ascending) */
     unsigned long long *deep_acc; /* listed segments << 32 | listed entries (zeroed per launch) */
-    uint32_t  *wide_next;     /* the wide kernel's next chunk of GB listed entries (zeroed per launch) */
+    uint32_t  *wide_next;     /* the group kernel's next chunk of GB listed entries (zeroed per launch) */
     uint32_t   deep_seg_cap;
     uint32_t   deep_nseg;     /* = main-kernel waves */
     uint32_t   deep_cap;      /* deep2 list capacity (>= n_sites: cannot overflow) */
-    uint32_t  *deep2_list;    /* sites the wide kernel cannot sort, any depth (ss_score_deep) */
+    uint32_t  *deep2_list;    /* sites the group kernel cannot sort, any depth (ss_score_deep) */
     uint32_t  *deep2_count;
     uint32_t  *err;           /* sticky error bits, see SS_KERR_* */
     ss_dev_model m;

@@ -741,7 +741,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
  * 4, then normal) both samples share one network ("joint"); otherwise the
  * tumor, then the normal is sorted and folded on its own ("separate").  Sites
  * with more than LN_N reads in a sample, malformed offsets, or a contributing
- * read of minq >= 64 (the 8-bit record holds q < 64) are listed for the wide
+ * read of minq >= 64 (the 8-bit record holds q < 64) are listed for the group
  * kernel (which hands the last two kinds on to the deep kernel).
  * ------------------------------------------------------------------------ */
 namespace {
@@ -859,7 +859,7 @@ __device__ __forceinline__ void ln_lut_build(uint2 *lut)
  * the per-sample rms sums and group sizes (four 8-bit fields, base b at 8b)
  * and the largest minq of any read (>= 64: the site needs 16-bit records).
  * Every x4 load stays inside the batch's reads (the caller routes a block that
- * would pass their end to the wide kernel); elements past a sample's reads are
+ * would pass their end to the group kernel); elements past a sample's reads are
  * zeroed, which makes them non-contributing (key 0xffff, rms 0). */
 struct LaneIn {
     const uint32_t *pa, *pb;         /* element e's read: pa + e (e < na4), pb + e (e >= na4) */
@@ -994,7 +994,7 @@ __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint2 *lut, u
 
 /* The sorted registers become fold records in place, two per register:
  * register r's elements r (low half) and 127 - r (high half, complemented)
- * give records q | strand << 6 (| 1 << 7 with WIDE: the wide fold's fsum
+ * give records q | strand << 6 (| 1 << 7 with WIDE: the group fold's fsum
  * multiplier, key_to_rec8) in bytes 0 and 2, computed on both halves at once
  * (q = max(minq, nz << 2), sniper_maqcns.c:165, for minq < 64 -- sites with a
  * larger one are not scored from these records).  Registers whose elements
@@ -1255,7 +1255,7 @@ void ss_score_main(ss_score_args a)
             in.tail = tail || __ballot((uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4);
             uint32_t v[LN_R];
             const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
-            /* a read of minq >= 64 needs 16-bit records: the wide kernel */
+            /* a read of minq >= 64 needs 16-bit records: the site goes to the group kernel */
             wild = wild || acc.maxq >= 64u;
             ln_levels<LN_R, 2>(v);
             ln_records(v, 4u * nch, L, lane);
@@ -1280,7 +1280,7 @@ void ss_score_main(ss_score_args a)
             wave_sync();                                     /* the pass's records are read */
         }
         ok = ok && !wild;
-        /* sites the lane path does not score: the wide kernel's list (one
+        /* sites the lane path does not score: the group kernel's list (one
          * segment per wave, no atomics) */
         const uint64_t out = __ballot(insite && !ok);
         if (out) {
@@ -1313,7 +1313,7 @@ void ss_score_main(ss_score_args a)
     }
     if (lane == 0 && ndeep) {
         /* one atomic numbers the segment and places its entries, so the
-         * offsets ascend with the segment index (the wide kernel searches them) */
+         * offsets ascend with the segment index (the group kernel searches them) */
         const ss_score_args &k = kernarg_args();
         const unsigned long long r = atomicAdd(k.deep_acc, 1ull << 32 | ndeep);
         k.deep_segs[r >> 32] = gw;
@@ -1340,9 +1340,9 @@ void ss_score_main(ss_score_args a)
  * descending U, so every unit sits in one wave-sized batch of lanes and its
  * lanes are aligned; a batch merges up to its largest U (lanes of smaller
  * units sit the larger levels out).  The sorted contributing keys leave as
- * the wide kernel's 8-bit fold records in the wave's arena, per unit in
- * ascending order, and the 16-site fold, likelihoods and decision are the wide
- * kernel's (finish_sub).
+ * 8-bit fold records in the wave's arena, per unit in
+ * ascending order, and finish_sub does the 16-site fold, likelihoods and
+ * decision.
  * ------------------------------------------------------------------------ */
 namespace {
 
@@ -1603,7 +1603,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
 }
 
 /* --------------------------------------------------------------------------
- * Deep kernel: the sites the wide kernel cannot sort (more than
+ * Deep kernel: the sites the group kernel cannot sort (more than
  * SS_WIDE_MAXSLOTS sort slots, any depth) and sites with malformed offsets.
  *
  * No sort: the fold only needs each (sample, base) group's reads in the
