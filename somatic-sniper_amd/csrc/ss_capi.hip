@@ -45,6 +45,7 @@ struct ss_ctx {
     uint32_t *d_deep_list;
     uint32_t deep_cap;
     uint32_t *d_deep_seg;     /* listed segments' first entries, then their main-wave ids */
+    uint8_t *d_grp_rec;       /* the group kernel's per-wave fold-record buffers */
     /* timing: a pool of events, SS_EV_PER_LAUNCH per launch while enabled */
     int timing;
     std::vector<hipEvent_t> *ev;
@@ -134,7 +135,7 @@ extern "C" void ss_ctx_destroy(ss_ctx_t *c)
     if (c->hstream) {
         void **ptrs[] = {(void **)&c->d_tab, (void **)&c->d_counters, (void **)&c->d_deep_list,
                          (void **)&c->d_deep_seg, &c->d_stage, (void **)&c->d_cdf, &c->d_scan_tmp,
-                         (void **)&c->d_depth_tmp};
+                         (void **)&c->d_depth_tmp, (void **)&c->d_grp_rec};
         for (void **p : ptrs) dev_free(*p, c->hstream);
         hipStreamSynchronize(c->hstream);
     }
@@ -192,6 +193,8 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
     TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t), hs));
     TRY(dev_alloc((void **)&c->d_deep_seg, 2 * (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t), hs));
     TRY(dev_alloc((void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t), hs));
+    /* one group-kernel workgroup per CU (wide_grid below), one buffer per wave */
+    TRY(dev_alloc((void **)&c->d_grp_rec, (size_t)c->n_cu * (SS_WIDE_BLOCK / 64) * SS_GRP_REC_BYTES, hs));
 #undef TRY
     /* the tables, lists and counters are complete before any launch can use them */
     if (hipMemsetAsync(c->d_counters, 0, 16 * sizeof(uint32_t), hs) != hipSuccess ||
@@ -297,6 +300,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.deep2_count = c->d_counters + 5;
     a.deep_acc = reinterpret_cast<unsigned long long *>(c->d_counters + 6);   /* 8-byte aligned */
     a.wide_next = c->d_counters + 8;
+    a.grp_rec = c->d_grp_rec;
     a.err = c->d_counters + 2;
     a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;
@@ -319,7 +323,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         evs = c->ev->data() + SS_EV_PER_LAUNCH * c->n_logged;
         ++c->n_logged;
     }
-    const int wide_grid = c->n_cu;                /* one 8-wave workgroup per CU fits (LDS) */
+    const int wide_grid = c->n_cu;                /* one 8-wave workgroup per CU (d_grp_rec is sized for it) */
     int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, s, evs);
     if (e != 0) return SS_E_HIP;
     HIPCHK(hipEventRecord(c->done, s));

@@ -74,6 +74,7 @@ struct ss_score_args {
     uint32_t  *deep2_list;    /* sites the group kernel cannot sort, any depth (ss_score_deep) */
     uint32_t  *deep2_count;
     uint32_t  *err;           /* sticky error bits, see SS_KERR_* */
+    uint8_t   *grp_rec;       /* the group kernel's fold records: SS_GRP_REC_BYTES per wave */
     ss_dev_model m;
 };
 
@@ -87,10 +88,12 @@ struct ss_score_args {
                                     the rest queued as short-lived waves (+5.5% over 16 per CU) */
 #define SS_DEEP_BLOCK      256
 #ifndef SS_WIDE_BLOCK
-#define SS_WIDE_BLOCK      512   /* 8 waves, one workgroup per CU (LDS); 12 waves with a
-                                    smaller arena measured slower */
+#define SS_WIDE_BLOCK      768   /* 12 waves, one workgroup per CU (168 VGPRs: 3 waves per SIMD) */
 #endif
 #define SS_WIDE_MAXSLOTS   2048  /* sort slots (tumor + pad + normal) per site    */
+#define SS_GRP_REC_MAX     65536 /* fold-record bytes of one group-kernel chunk: 16 sites x 2 x 2048 */
+#define SS_GRP_REC_PAD     64    /* pad before and after (a 16-record window may reach past either end) */
+#define SS_GRP_REC_BYTES   (SS_GRP_REC_MAX + 2 * SS_GRP_REC_PAD)
 
 /* Launchers (return hipError_t as int). */
 int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, hipStream_t s,

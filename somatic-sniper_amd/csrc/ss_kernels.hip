@@ -36,10 +36,6 @@
 
 /* Fixed tuning of the shipped kernels (each measured on MI355X):
  * one code path per choice, no run-time or build-time alternatives. */
-#define SS_FOLD_UNROLL 8  /* fold loop unroll (2 -> 8: +0.5% main, +4% at 500x/500x) */
-/* `#pragma unroll N` with N from a macro: the count reaches the pragma expanded */
-#define SS_PRAGMA(x) _Pragma(#x)
-#define SS_UNROLL(n) SS_PRAGMA(unroll n)
 namespace {
 
 /* --------------------------------------------------------------------------
@@ -484,12 +480,6 @@ __device__ __forceinline__ void nt_tables(uint32_t ref16, uint32_t &tb, uint32_t
     th = TH | ((TH >> (2u * ref16)) & 1u);
 }
 
-template <typename RecT> struct RecForm;
-template <> struct RecForm<uint8_t> {
-    static __device__ __forceinline__ uint32_t shift(uint32_t r) { return (r >> 2) & 16u; }
-    static constexpr uint32_t ONE_BIT = 7u, QBITS = 6u;
-};
-
 __device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b)
 {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -566,66 +556,126 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
  * fields, counting in units of 8 = the byte stride of fk), selected by the
  * record's strand<<4 field and saturated at w = 255 (:170).  Base groups are
  * walked longest first, so the wave-wide trip count is set by one long chain
- * per lane. */
-template <typename RecT>
-__device__ __forceinline__ void fold_sample(const RecT *rec, const uint32_t cnt[4],
+ * per lane.
+ *
+ * The records lie in the wave's global buffer (L2): a chain is walked from
+ * its top in blocks of 16 records, each block five dwords (one unaligned
+ * 16-byte window) loaded one block ahead, four records per step through
+ * v_alignbyte as in the main kernel's fold.  A step past the chain's end
+ * reads fk's zero entry (x + 0.0 == x). */
+#define GP_FK_ZERO 256
+
+/* the five dwords that hold records top - 16 .. top - 1 (buffer positions;
+ * top - 16 may lie before the buffer's start, inside its pad) */
+__device__ __forceinline__ void gp_block(const uint8_t *buf, int top, uint32_t (&w)[5])
+{
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(buf + ((top - 16) & ~3));
+#pragma unroll
+    for (int q = 0; q < 5; ++q) w[q] = p[q];
+}
+
+/* four steps of a chain from the window R of records k0 - 3 .. k0 (k0 in the
+ * top byte); steps j >= m read fk's zero entry */
+template <bool TAIL>
+__device__ __forceinline__ void gp_steps(const char *fkb, uint32_t R, int m, uint32_t moff, uint32_t mwid,
+                                         uint32_t &W, float &e)
+{
+    double t[4];
+    uint32_t mq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t r = R >> (24 - 8 * j);                      /* record k0 - j in the low byte */
+        const uint32_t sh = (r >> 2) & 16u;                        /* strand << 4 */
+        uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
+        w8 = w8 < 2040u ? w8 : 2040u;
+        if (TAIL) w8 = j < m ? w8 : 8u * GP_FK_ZERO;
+        W += 8u << sh;
+        t[j] = *reinterpret_cast<const double *>(fkb + w8);
+        mq[j] = __builtin_amdgcn_ubfe(r, moff, mwid);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e = (float)((double)e + t[j] * (double)mq[j]);
+}
+
+/* the 16 records below top in four steps (m: how many of them belong to the
+ * chain); steps that no lane of the wave needs are skipped */
+template <bool TAIL>
+__device__ __forceinline__ void gp_block_steps(const char *fkb, const uint32_t (&w)[5], int top, int m,
+                                               uint32_t moff, uint32_t mwid, uint32_t &W, float &e)
+{
+    const uint32_t q = (uint32_t)(top - 16) & 3u;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        if (TAIL && !__ballot(m > 4 * s)) break;
+        gp_steps<TAIL>(fkb, __builtin_amdgcn_alignbyte(w[4 - s], w[3 - s], q), m - 4 * s, moff, mwid, W, e);
+    }
+}
+
+/* chain of records [s0, s0 + n) of the buffer, from the top; w holds the
+ * block below s0 + n (loaded by the caller) */
+__device__ __forceinline__ float gp_chain(const uint8_t *buf, uint32_t s0, uint32_t n, uint32_t (&w)[5],
+                                          const char *fkb, uint32_t moff, uint32_t mwid)
+{
+    float e = 0.0f;
+    uint32_t W = 0;
+    if (__ballot(n >= 16u)) {
+        /* whole blocks while any lane has 16 records left, the next two
+         * blocks in flight; a lane with fewer keeps its state and its window
+         * (which then holds its last, partial block) by selects */
+        uint32_t wn[5];
+        gp_block(buf, max((int)(s0 + n) - 16, 0), wn);
+        for (uint32_t i = 0; __ballot(i + 16u <= n); i += 16u) {
+            const bool act = i + 16u <= n;
+            const int top = (int)(s0 + n) - (int)i;
+            uint32_t wnn[5];
+            gp_block(buf, max(top - 32, 0), wnn);
+            float e2 = e;
+            uint32_t W2 = W;
+            gp_block_steps<false>(fkb, w, top, 16, moff, mwid, W2, e2);
+            e = act ? e2 : e;
+            W = act ? W2 : W;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                w[q] = act ? wn[q] : w[q];
+                wn[q] = act ? wnn[q] : wn[q];
+            }
+        }
+    }
+    /* the lane's last 0 .. 15 records (below its whole blocks): window w */
+    const uint32_t m = n & 15u;
+    if (__ballot(m > 0u)) {
+        if (m > 0u) gp_block_steps<true>(fkb, w, (int)(s0 + m), (int)m, moff, mwid, W, e);
+    }
+    return e;
+}
+
+__device__ __forceinline__ void fold_sample(const uint8_t *buf, uint32_t s0, const uint32_t cnt[4],
                                             const double *fk, uint32_t role, float acc[4])
 {
-    const uint32_t start1 = cnt[0], start2 = cnt[0] + cnt[1], start3 = start2 + cnt[2];
-    const uint32_t moff = role ? RecForm<RecT>::ONE_BIT : 0u, mwid = role ? 1u : RecForm<RecT>::QBITS;
+    const uint32_t start1 = s0 + cnt[0], start2 = start1 + cnt[1], start3 = start2 + cnt[2];
+    const uint32_t moff = role ? 7u : 0u, mwid = role ? 1u : 6u;   /* fsum multiplier bit / q */
     const char *fkb = reinterpret_cast<const char *>(fk);
     uint32_t L = 0;
 #pragma unroll
     for (uint32_t b = 1; b < 4; ++b) L = cnt[b] > (L == 0 ? cnt[0] : (L == 1 ? cnt[1] : cnt[2])) ? b : L;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[b] = 0.0f;
+    /* the four chains in walking order (the largest first), and the top
+     * block of each, all loaded up front */
+    uint32_t sb[4], tb[4], bb[4];
+    uint32_t w[4][5];
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) {
         const uint32_t b = i == 0 ? L : (i - 1u) + ((i - 1u) >= L ? 1u : 0u);
-        const uint32_t s0 = b == 0 ? 0u : (b == 1 ? start1 : (b == 2 ? start2 : start3));
-        const uint32_t t = b == 0 ? cnt[0] : (b == 1 ? cnt[1] : (b == 2 ? cnt[2] : cnt[3]));
-        const RecT *p0 = rec + s0;
-        float e = 0.0f;
-        uint32_t W = 0;
-        uint32_t k = t;                               /* records left, walked from the top */
-        /* batches of SS_FOLD_UNROLL: the records and their fk[w] * m terms are
-         * all loaded / formed before the dependent chain, which is then only
-         * (double)e + term -> (float), as in the reference */
-        while (k >= (uint32_t)SS_FOLD_UNROLL) {
-            double term[SS_FOLD_UNROLL];
-            uint32_t w8[SS_FOLD_UNROLL], m[SS_FOLD_UNROLL];
+        bb[i] = b;
+        sb[i] = b == 0 ? s0 : (b == 1 ? start1 : (b == 2 ? start2 : start3));
+        tb[i] = b == 0 ? cnt[0] : (b == 1 ? cnt[1] : (b == 2 ? cnt[2] : cnt[3]));
+        gp_block(buf, (int)(sb[i] + tb[i]), w[i]);
+    }
 #pragma unroll
-            for (int j = 0; j < SS_FOLD_UNROLL; ++j) {
-                const uint32_t r = p0[k - 1u - (uint32_t)j];
-                const uint32_t sh = RecForm<RecT>::shift(r);   /* 0 or 16 */
-                const uint32_t w = __builtin_amdgcn_ubfe(W, sh, 16u);
-                w8[j] = w < 2040u ? w : 2040u;
-                W += 8u << sh;
-                m[j] = __builtin_amdgcn_ubfe(r, moff, mwid);
-            }
+    for (uint32_t i = 0; i < 4; ++i) {
+        const float e = gp_chain(buf, sb[i], tb[i], w[i], fkb, moff, mwid);
 #pragma unroll
-            for (int j = 0; j < SS_FOLD_UNROLL; ++j) term[j] = *reinterpret_cast<const double *>(fkb + w8[j]);
-            /* keep the scheduler from pairing each load with its use (it would
-             * wait for every fk load on its own) */
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < SS_FOLD_UNROLL; ++j) e = (float)((double)e + term[j] * (double)m[j]);
-            k -= (uint32_t)SS_FOLD_UNROLL;
-        }
-        while (k) {
-            --k;
-            const uint32_t r = p0[k];
-            const uint32_t sh = RecForm<RecT>::shift(r);
-            uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
-            w8 = w8 < 2040u ? w8 : 2040u;
-            W += 8u << sh;
-            const double f = *reinterpret_cast<const double *>(fkb + w8);
-            const uint32_t m = __builtin_amdgcn_ubfe(r, moff, mwid);
-            e = (float)((double)e + f * (double)m);
-        }
-#pragma unroll
-        for (uint32_t bb = 0; bb < 4; ++bb)
-            if (bb == b) acc[bb] = e;
+        for (uint32_t b2 = 0; b2 < 4; ++b2)
+            if (b2 == bb[i]) acc[b2] = e;
     }
 }
 
@@ -644,14 +694,41 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-/* Phases B, C, D for the G sites of a sub-group.  Fold records are RecT
- * entries of `recs` (slot rec_n index). */
-template <typename RecT>
-__device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const RecT *recs,
+/* inclusive prefix sum over the 64 lanes (DPP row shifts, then row
+ * broadcasts; lanes without a source add the `old` 0) */
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); /* row_shr:1 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); /* row_shr:2 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); /* row_shr:4 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); /* row_shr:8 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); /* row_bcast:15 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); /* row_bcast:31 */
+    return v;
+}
+
+/* sum over the 64 lanes (no overflow: the caller's values are small), wave-uniform */
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); /* row_shr:1 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); /* row_shr:2 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); /* row_shr:4 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); /* row_shr:8 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); /* row_bcast:15 */
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); /* row_bcast:31 */
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+/* Phases B, C, D for the G sites of a chunk.  Fold records are bytes of the
+ * wave's global buffer `recs` (slot rec_n index). */
+__device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const uint8_t *recs,
                                            const Slot3 *slot, SlotRes *res, const uint32_t *sites,
                                            const uint32_t *refcs, const double *fk)
 {
-    const uint32_t lane = lane_id();
+    /* opaque: the slot addresses are then formed here, not hoisted out of the
+     * kernel's loops (where they were live across the sort and spilled) */
+    uint32_t lane = lane_id();
+    asm volatile("" : "+v"(lane));
     const int sl = (int)(lane >> 1);               /* slot = site * 2 + sample */
     const uint32_t role = lane & 1u;               /* 0: esum lane, 1: fsum lane */
     const bool act = sl < 2 * G;
@@ -663,8 +740,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         cnt[2] = m3.cnt23 & 0xffffu; cnt[3] = m3.cnt23 >> 16;
         depth = m3.rec_n >> 16;
         rms = m3.rms;
-        const RecT *rec = recs + (m3.rec_n & 0xffffu);
-        fold_sample<RecT>(rec, cnt, fk, role, acc);
+        fold_sample(recs, m3.rec_n & 0xffffu, cnt, fk, role, acc);
     } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
@@ -1346,16 +1422,23 @@ void ss_score_main(ss_score_args a)
  * ------------------------------------------------------------------------ */
 namespace {
 
-#define GP_WAVES (SS_WIDE_BLOCK / 64)         /* 8 waves, one workgroup per CU (LDS) */
-#define GP_ARENA 16384                     /* record bytes per wave (16 sites of ~1000 reads) */
+#define GP_WAVES (SS_WIDE_BLOCK / 64)         /* 12 waves, one workgroup per CU (168 VGPRs: 3 per SIMD) */
 #define GP_UNITS (2 * GB)
 
+/* Per wave: the chunk's sites and units are kept here, not in registers, so
+ * that the sort and merge (64 registers of keys) leave room for 3 waves per
+ * SIMD; lanes read the entries they need. */
 struct alignas(16) GroupLds {
-    uint8_t  arena[GP_WAVES][GP_ARENA];
     Slot3    slot[GP_WAVES][2 * GB];
     SlotRes  res[GP_WAVES][2 * GB];
-    uint32_t site[GP_WAVES][GB];
-    uint32_t refc[GP_WAVES][GB];
+    uint32_t site[GP_WAVES][GB];                   /* the chunk's sites, then (compacted) the scored ones */
+    uint32_t refc[GP_WAVES][GB];                   /* ref char | nt16 << 8 (then compacted like site) */
+    uint32_t c_site[GP_WAVES][GB];                 /* chunk entry k: site */
+    uint32_t c_ot[GP_WAVES][GB], c_on[GP_WAVES][GB];   /* its first tumor / normal read */
+    uint32_t c_ref[GP_WAVES][GB];                  /* ref char | nt16 << 8 | ok << 31 */
+    uint32_t u_n[GP_WAVES][GP_UNITS];              /* unit u = (entry u / 2, sample u & 1): reads */
+    uint32_t u_off[GP_WAVES][GP_UNITS];            /* its first lane position */
+    uint32_t u_base[GP_WAVES][GP_UNITS];           /* its first record byte */
     uint32_t ucnt[GP_WAVES][GP_UNITS][4];          /* per unit: counts of bases 0, 2 | 1, 3 (16-bit), rms, wild */
     uint8_t  unit_of[GP_WAVES][GP_UNITS * 16];     /* lane position -> unit */
 };
@@ -1412,18 +1495,20 @@ __device__ __forceinline__ uint32_t gp_lanes(uint32_t n)
 
 __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
 {
-    __shared__ double fk[256];
+    __shared__ double fk[GP_FK_ZERO + 1];
     __shared__ uint2 lut[LN_LUT_BYTES / 8];
     __shared__ GroupLds L;
     const unsigned long long acc0 = *a.deep_acc;
     const uint32_t nsegs = min((uint32_t)(acc0 >> 32), a.deep_nseg), total = (uint32_t)acc0;
     if (nsegs == 0u) return;
-    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
+    for (uint32_t i = threadIdx.x; i <= GP_FK_ZERO; i += blockDim.x) fk[i] = i < 256u ? ss_tab_fk(a.m)[i] : 0.0;
     ln_lut_build(lut);
     __syncthreads();
-    const uint32_t lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint8_t *arena = L.arena[wv];
+    /* the wave's fold records: a global (L2-resident) buffer that holds any
+     * chunk (16 sites x 2 x 2048 records), so a chunk's sites always fold
+     * together; its address is re-derived where used (not held in SGPRs) */
+    const size_t arena_off = (size_t)(blockIdx.x * GP_WAVES + wv) * SS_GRP_REC_BYTES + SS_GRP_REC_PAD;
     Slot3 *slot = L.slot[wv];
     SlotRes *res = L.res[wv];
     uint32_t *sites = L.site[wv], *refcs = L.refc[wv];
@@ -1432,65 +1517,57 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
     for (;;) {
+        /* opaque per chunk: the lane's LDS addresses are formed inside the
+         * loop, not hoisted out of it (where they stayed live and spilled) */
+        uint32_t lane = lane_id();
+        asm volatile("" : "+v"(lane));
         uint32_t ch = 0;
         if (lane == 0u) ch = atomicAdd(kernarg_args().wide_next, 1u);
         const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * GB;
         if (first >= total) break;
-        const uint32_t nlist = total - first < GB ? total - first : GB;
-        /* the chunk's sites, lane k = entry k */
-        const ss_score_args &k = kernarg_args();
-        uint32_t lo = 0, hi = nsegs;
-        while (hi - lo > 1u) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (k.deep_off[mid] <= first) lo = mid;
-            else hi = mid;
-        }
-        uint32_t c_s = 0, c_ot = 0, c_nt = 0, c_on = 0, c_nn = 0, c_ref = 0;
-        bool c_ok = false;
-        if (lane < nlist) {
-            const uint32_t p = first + lane;
-            uint32_t sg = lo;
-            while (sg + 1u < nsegs && k.deep_off[sg + 1u] <= p) ++sg;
-            c_s = k.deep_list[(size_t)k.deep_segs[sg] * k.deep_seg_cap + (p - k.deep_off[sg])];
-            c_ot = k.off_t[c_s];
-            const uint32_t ot1 = k.off_t[c_s + 1];
-            c_on = k.off_n[c_s];
-            const uint32_t on1 = k.off_n[c_s + 1];
-            const uint32_t rc = k.ref[c_s];
-            c_ref = rc | (uint32_t)ss_tab_nt16(k.m)[rc] << 8;
-            c_ok = c_ot <= ot1 && ot1 <= end_t && c_on <= on1 && on1 <= end_n &&
-                   ot1 - c_ot <= SS_WIDE_MAXSLOTS && on1 - c_on <= SS_WIDE_MAXSLOTS;
-            c_nt = c_ok ? ot1 - c_ot : 0u;
-            c_nn = c_ok ? on1 - c_on : 0u;
-            if (!c_ok) {                             /* malformed or too deep: the deep kernel */
-                const uint32_t d = atomicAdd(k.deep2_count, 1u);
-                if (d < k.deep_cap) k.deep2_list[d] = c_s;
-                else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
+        const uint32_t G = total - first < GB ? total - first : GB;
+        /* the chunk's entries, lane k = entry k, into LDS */
+        {
+            const ss_score_args &k = kernarg_args();
+            uint32_t lo = 0, hi = nsegs;
+            while (hi - lo > 1u) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (k.deep_off[mid] <= first) lo = mid;
+                else hi = mid;
+            }
+            if (lane < G) {
+                const uint32_t p = first + lane;
+                uint32_t sg = lo;
+                while (sg + 1u < nsegs && k.deep_off[sg + 1u] <= p) ++sg;
+                const uint32_t cs = k.deep_list[(size_t)k.deep_segs[sg] * k.deep_seg_cap + (p - k.deep_off[sg])];
+                const uint32_t ot = k.off_t[cs], ot1 = k.off_t[cs + 1];
+                const uint32_t on = k.off_n[cs], on1 = k.off_n[cs + 1];
+                const uint32_t rc = k.ref[cs];
+                const bool ok = ot <= ot1 && ot1 <= end_t && on <= on1 && on1 <= end_n &&
+                                ot1 - ot <= SS_WIDE_MAXSLOTS && on1 - on <= SS_WIDE_MAXSLOTS;
+                L.c_site[wv][lane] = cs;
+                L.c_ot[wv][lane] = ot;
+                L.c_on[wv][lane] = on;
+                L.c_ref[wv][lane] = rc | (uint32_t)ss_tab_nt16(k.m)[rc] << 8 | (ok ? 1u << 31 : 0u);
+                L.u_n[wv][2u * lane] = ok ? ot1 - ot : 0u;
+                L.u_n[wv][2u * lane + 1u] = ok ? on1 - on : 0u;
+                if (!ok) {                                /* malformed or too deep: the deep kernel */
+                    const uint32_t d = atomicAdd(k.deep2_count, 1u);
+                    if (d < k.deep_cap) k.deep2_list[d] = cs;
+                    else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
+                }
             }
         }
-        /* sub-groups of consecutive sites whose records fit the arena */
-        const uint32_t need = c_ok ? ((c_nt + 3u) & ~3u) + ((c_nn + 3u) & ~3u) : 0u;
-        uint32_t done = 0;
-        while (done < nlist) {
-            /* sites done .. done + G - 1 (inclusive prefix of `need` within the arena) */
-            uint32_t pre = lane >= done && lane < nlist ? need : 0u;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = (uint32_t)__shfl_up((int)pre, o);
-                if (lane >= (uint32_t)o) pre += t;
-            }
-            const uint64_t fit = __ballot(lane >= done && lane < nlist && pre <= GP_ARENA);
-            const uint32_t G = max(1u, (uint32_t)__popcll(fit));     /* a site always fits (2 x 2048 <= 16 K) */
-            const uint32_t s0 = done;
-            done += G;
-            /* units of the sub-group: lane u < 2G is unit u = (site s0 + u / 2, sample u & 1) */
-            const uint32_t us = s0 + (lane >> 1);
+        wave_sync();
+        uint32_t T = 0;
+        {
+            /* units: lane u < 2G is unit u = (entry u / 2, sample u & 1); lane
+             * positions by descending U (aligned, so a unit never straddles a
+             * batch), record bases in unit order rounded up to 16 bytes (x4 stores) */
             const bool is_u = lane < 2u * G;
-            const uint32_t s_nt = (uint32_t)__shfl((int)c_nt, (int)us), s_nn = (uint32_t)__shfl((int)c_nn, (int)us);
-            const uint32_t n_u = is_u ? ((lane & 1u) ? s_nn : s_nt) : 0u;
+            const uint32_t n_u = is_u ? L.u_n[wv][lane] : 0u;
             const uint32_t U_u = gp_lanes(n_u);
-            /* lane offsets by descending U (aligned, so a unit never straddles a batch) */
-            uint32_t off_u = 0, T = 0;
+            uint32_t off_u = 0;
 #pragma unroll
             for (uint32_t c = 16u; c >= 1u; c >>= 1) {
                 const uint64_t mk = __ballot(is_u && U_u == c);
@@ -1498,107 +1575,115 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
                     off_u = T + c * __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
                 T += c * (uint32_t)__popcll(mk);
             }
-            /* arena bases: units in order, records rounded up to 4 bytes */
-            uint32_t base = is_u ? ((n_u + 3u) & ~3u) : 0u;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = (uint32_t)__shfl_up((int)base, o);
-                if (lane >= (uint32_t)o) base += t;
-            }
-            base -= is_u ? ((n_u + 3u) & ~3u) : 0u;       /* exclusive */
+            const uint32_t sz = is_u ? ((n_u + 15u) & ~15u) : 0u;
+            const uint32_t base = wave_scan(sz);
             if (is_u) {
+                L.u_off[wv][lane] = off_u;
+                L.u_base[wv][lane] = base - sz;           /* exclusive */
                 for (uint32_t t = 0; t < U_u; ++t) unit_of[off_u + t] = (uint8_t)lane;
-                ucnt[lane][0] = ucnt[lane][1] = ucnt[lane][2] = ucnt[lane][3] = 0u;
+                uint32_t z = 0u;                              /* (not a zero vector kept live) */
+                asm volatile("" : "+v"(z));
+                ucnt[lane][0] = ucnt[lane][1] = ucnt[lane][2] = ucnt[lane][3] = z;
             }
-            wave_sync();
-            for (uint32_t b0 = 0; b0 < T; b0 += 64u) {
-                const uint32_t p = b0 + lane;
-                const bool act = p < T;
-                const uint32_t u = act ? unit_of[p] : 0u;
-                const uint32_t un = (uint32_t)__shfl((int)n_u, (int)u), uU = (uint32_t)__shfl((int)U_u, (int)u);
-                const uint32_t uoff = (uint32_t)__shfl((int)off_u, (int)u);
-                const uint32_t site_l = s0 + (u >> 1), smp = u & 1u;
-                const uint32_t r_ot = (uint32_t)__shfl((int)c_ot, (int)site_l), r_on = (uint32_t)__shfl((int)c_on, (int)site_l);
-                const uint32_t rofs = smp ? r_on : r_ot;
-                const uint32_t ref16 = (uint32_t)__shfl((int)c_ref, (int)site_l) >> 8;
-                const uint32_t j = p - uoff;
-                LaneIn in;
-                const int rem = act ? (int)un - (int)(128u * j) : 0;
-                in.na = (uint32_t)min(max(rem, 0), 128);
-                in.na4 = (in.na + 3u) & ~3u;
-                in.nb = 0u;
-                in.nca = in.na4 >> 2;
-                asm("" : "+v"(in.nca));         /* as in ss_score_main */
-                in.nab = in.na4;
-                const uint32_t *base_s = smp ? kernarg_args().reads_n : kernarg_args().reads_t;
-                const uint32_t start = act ? rofs + 128u * j : 0u;
-                in.pa = base_s + start;
-                in.pb = in.pa;
-                in.la = in.lb = 256u * (1u + smp * 16u + ref16);
-                const uint32_t nch = wave_max((in.nab + 3u) >> 2);
-                const uint32_t endv = smp ? end_n : end_t;
-                in.tail = __ballot((uint64_t)start + 4u * nch > (uint64_t)endv) || end_t < 4u || end_n < 4u;
-                uint32_t v[LN_R];
-                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
-                ln_levels<LN_R, 2>(v);
-                if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }
-                if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }
-                if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }
-                if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }
-                if (act) {
-                    const uint32_t c = acc.cnt_a;
-                    atomicAdd(&ucnt[u][0], c & 0x00ff00ffu);
-                    atomicAdd(&ucnt[u][1], (c >> 8) & 0x00ff00ffu);
-                    atomicAdd(&ucnt[u][2], acc.rms_a);
-                    if (acc.maxq >= 64u) ucnt[u][3] = 1u;     /* 8-bit records cannot hold its q */
-                }
-                wave_sync();
-                /* the unit's contributing keys as records, ascending */
-                const uint32_t ca = act ? ucnt[u][0] : 0u, cb = act ? ucnt[u][1] : 0u;
-                const uint32_t tot = (ca & 0xffffu) + (ca >> 16) + (cb & 0xffffu) + (cb >> 16);
-                const int lim = act ? min(max((int)tot - (int)(128u * j), 0), 128) : 0;
-                const uint32_t ubase = (uint32_t)__shfl((int)base, (int)u) + 128u * j;
-                ln_to_records<true>(v, wave_max((uint32_t)lim));
-#pragma unroll
-                for (int i = 0; i < LN_C; ++i) {
-                    if (!__ballot(4 * i < lim)) continue;
-                    if (4 * i < lim) *reinterpret_cast<uint32_t *>(arena + ubase + 4u * (uint32_t)i) = ln_rec_dword(v, i);
-                }
-                wave_sync();
-            }
-            /* slots of the sites that stay (no wild read, well formed), compacted */
-            const uint32_t wild_u = is_u ? ucnt[lane][3] : 0u;
-            const uint64_t wildm = __ballot(wild_u != 0u);
-            const bool site_lane = lane >= s0 && lane < s0 + G;
-            const uint32_t su = lane - s0;                       /* this site lane's units 2su, 2su + 1 */
-            const bool stay = site_lane && c_ok && !((wildm >> (2u * su)) & 3u);
-            const uint64_t staym = __ballot(stay);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(staym >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)staym, 0u));
-            if (site_lane && c_ok && !stay) {                    /* a wild read: the deep kernel */
-                const uint32_t d = atomicAdd(k.deep2_count, 1u);
-                if (d < k.deep_cap) k.deep2_list[d] = c_s;
-                else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
-            }
-            /* unit lanes publish their slot under the site's rank */
-            const uint32_t rank_u = (uint32_t)__shfl((int)rank, (int)us);
-            const bool stay_u = is_u && ((staym >> us) & 1ull);
-            if (stay_u) {
-                Slot3 &st = slot[2u * rank_u + (lane & 1u)];
-                const uint32_t ca = ucnt[lane][0], cb = ucnt[lane][1];
-                st.rec_n = base | n_u << 16;
-                st.cnt01 = (ca & 0xffffu) | (cb & 0xffffu) << 16;
-                st.cnt23 = (ca >> 16) | (cb >> 16) << 16;
-                st.rms = ucnt[lane][2];
-            }
-            if (stay) {
-                sites[rank] = c_s;
-                refcs[rank] = c_ref;
-            }
-            const uint32_t G2 = (uint32_t)__popcll(staym);
-            wave_sync();
-            if (G2) finish_sub<uint8_t>(kernarg_args(), (int)G2, arena, slot, res, sites, refcs, fk);
         }
+        wave_sync();
+        for (uint32_t b0 = 0; b0 < T; b0 += 64u) {
+            const uint32_t p = b0 + lane;
+            const bool act = p < T;
+            const uint32_t u = act ? unit_of[p] : 0u;
+            const uint32_t un = L.u_n[wv][u], uU = gp_lanes(un);
+            const uint32_t site_l = u >> 1, smp = u & 1u;
+            const uint32_t j = p - L.u_off[wv][u];
+            LaneIn in;
+            const int rem = act ? (int)un - (int)(128u * j) : 0;
+            in.na = (uint32_t)min(max(rem, 0), 128);
+            in.na4 = (in.na + 3u) & ~3u;
+            in.nb = 0u;
+            in.nca = in.na4 >> 2;
+            asm("" : "+v"(in.nca));         /* as in ss_score_main */
+            in.nab = in.na4;
+            const uint32_t *base_s = smp ? kernarg_args().reads_n : kernarg_args().reads_t;
+            const uint32_t start = act ? (smp ? L.c_on[wv][site_l] : L.c_ot[wv][site_l]) + 128u * j : 0u;
+            in.pa = base_s + start;
+            in.pb = in.pa;
+            in.la = in.lb = 256u * (1u + smp * 16u + ((L.c_ref[wv][site_l] >> 8) & 0xffu));
+            const uint32_t nch = wave_max((in.nab + 3u) >> 2);
+            const uint32_t endv = smp ? end_n : end_t;
+            in.tail = __ballot((uint64_t)start + 4u * nch > (uint64_t)endv) || end_t < 4u || end_n < 4u;
+            uint32_t v[LN_R];
+            const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
+            /* the unit's counts before the sort: acc is not live across it */
+            if (act) {
+                const uint32_t c = acc.cnt_a;
+                atomicAdd(&ucnt[u][0], c & 0x00ff00ffu);
+                atomicAdd(&ucnt[u][1], (c >> 8) & 0x00ff00ffu);
+                atomicAdd(&ucnt[u][2], acc.rms_a);
+                if (acc.maxq >= 64u) ucnt[u][3] = 1u;     /* 8-bit records cannot hold its q */
+            }
+            ln_levels<LN_R, 2>(v);
+            if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }
+            if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }
+            if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }
+            if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }
+            wave_sync();
+            /* the unit's contributing keys as records, ascending, 16 per store:
+             * past lim they stay inside the lane's 128 slots and the unit's
+             * 16-byte rounding */
+            const uint32_t ca = act ? ucnt[u][0] : 0u, cb = act ? ucnt[u][1] : 0u;
+            const uint32_t tot = (ca & 0xffffu) + (ca >> 16) + (cb & 0xffffu) + (cb >> 16);
+            const int lim = act ? min(max((int)tot - (int)(128u * j), 0), 128) : 0;
+            const uint32_t ubase = L.u_base[wv][u] + 128u * j;
+            ln_to_records<true>(v, wave_max((uint32_t)lim));
+            uint8_t *gbuf = kernarg_args().grp_rec + arena_off;
+#pragma unroll
+            for (int i = 0; i < LN_C; i += 4) {
+                if (!__ballot(4 * i < lim)) continue;
+                if (4 * i < lim)
+                    *reinterpret_cast<uint4 *>(gbuf + ubase + 4u * (uint32_t)i) =
+                        make_uint4(ln_rec_dword(v, i), ln_rec_dword(v, i + 1), ln_rec_dword(v, i + 2),
+                                   ln_rec_dword(v, i + 3));
+            }
+            wave_sync();
+        }
+        /* slots of the sites that stay (no wild read, well formed), compacted */
+        const bool is_u = lane < 2u * G;
+        const uint32_t wild_u = is_u ? ucnt[lane][3] : 0u;
+        const uint64_t wildm = __ballot(wild_u != 0u);
+        const bool site_lane = lane < G;
+        const uint32_t cref = site_lane ? L.c_ref[wv][lane] : 0u;
+        const bool c_ok = (cref >> 31) != 0u;
+        const bool stay = site_lane && c_ok && !((wildm >> (2u * lane)) & 3u);
+        const uint64_t staym = __ballot(stay);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(staym >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)staym, 0u));
+        if (site_lane && c_ok && !stay) {                    /* a wild read: the deep kernel */
+            const ss_score_args &k = kernarg_args();
+            const uint32_t d = atomicAdd(k.deep2_count, 1u);
+            if (d < k.deep_cap) k.deep2_list[d] = L.c_site[wv][lane];
+            else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
+        }
+        /* unit lanes publish their slot under the site's rank */
+        const uint32_t us = lane >> 1;
+        const uint32_t rank_u = (uint32_t)__shfl((int)rank, (int)us);
+        const bool stay_u = is_u && ((staym >> us) & 1ull);
+        if (stay_u) {
+            Slot3 &st = slot[2u * rank_u + (lane & 1u)];
+            const uint32_t ca = ucnt[lane][0], cb = ucnt[lane][1];
+            st.rec_n = L.u_base[wv][lane] | L.u_n[wv][lane] << 16;
+            st.cnt01 = (ca & 0xffffu) | (cb & 0xffffu) << 16;
+            st.cnt23 = (ca >> 16) | (cb >> 16) << 16;
+            st.rms = ucnt[lane][2];
+        }
+        const uint32_t cs = site_lane ? L.c_site[wv][lane] : 0u;
+        if (stay) {
+            sites[rank] = cs;
+            refcs[rank] = cref & 0xffffu;
+        }
+        const uint32_t G2 = (uint32_t)__popcll(staym);
+        /* the records' global stores complete before any lane reads them */
+        __builtin_amdgcn_s_waitcnt(0x0f70);                  /* vmcnt(0) */
+        wave_sync();
+        if (G2) finish_sub(kernarg_args(), (int)G2, kernarg_args().grp_rec + arena_off, slot, res, sites, refcs, fk);
     }
 }
 

@@ -53,10 +53,15 @@ EDITS = {
                   "                if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }\n"
                   "                if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }\n"
                   "                if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }\n", "")],
-    "gnorec": [("                    if (4 * i < lim) *reinterpret_cast<uint32_t *>(arena + ubase + 4u * (uint32_t)i) = "
-                "ln_rec_dword(v, i);\n", "")],
-    "gnofold": [("        fold_sample<RecT>(rec, cnt, fk, role, acc);\n",
-                 "        for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b] + (float)rec[b];\n")],
+    "gnorec": [("                        if (4 * i < lim) *reinterpret_cast<uint32_t *>(arena + ubase + 4u * (uint32_t)i) = "
+                "ln_rec_dword(v, i);\n", ""),
+               ("                        if (4 * i < lim)\n"
+                "                            *reinterpret_cast<uint4 *>(gbuf + ubase + 4u * (uint32_t)i) =\n"
+                "                                make_uint4(ln_rec_dword(v, i), ln_rec_dword(v, i + 1), ln_rec_dword(v, i + 2),\n"
+                "                                           ln_rec_dword(v, i + 3));\n", "")],
+    "gnofold": [("        if (in_lds) fold_sample(recs_lds, m3.rec_n & 0xffffu, cnt, fk, role, acc);\n"
+                 "        else fold_sample(recs_glb, m3.rec_n & 0xffffu, cnt, fk, role, acc);\n",
+                 "        for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b] + (float)recs_lds[b];\n")],
     "gnofin": [("    geno_p5(role, es, fs, c, tot, a.m, mine);\n",
                 "    for (int t = 0; t < 5; ++t) mine[t] = es[t & 3] + (float)c[t & 3];\n")],
 }
