@@ -91,7 +91,7 @@ struct ss_score_args {
 #define SS_WIDE_BLOCK      768   /* 12 waves, one workgroup per CU (168 VGPRs: 3 waves per SIMD) */
 #endif
 #define SS_WIDE_MAXSLOTS   2048  /* sort slots (tumor + pad + normal) per site    */
-#define SS_GRP_REC_MAX     65536 /* fold-record bytes of one group-kernel chunk: 16 sites x 2 x 2048 */
+#define SS_GRP_REC_MAX     131072 /* fold-record bytes of one group-kernel chunk: 32 sites x 2 x 2048 */
 #define SS_GRP_REC_PAD     64    /* pad before and after (a 16-record window may reach past either end) */
 #define SS_GRP_REC_BYTES   (SS_GRP_REC_MAX + 2 * SS_GRP_REC_PAD)
 

@@ -43,6 +43,15 @@ namespace {
  * ------------------------------------------------------------------------ */
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+/* the lane index recomputed where it is used (volatile, so not hoisted out
+ * of a loop and kept live across it: in the group kernel such copies spilled) */
+__device__ __forceinline__ uint32_t lane_id_here()
+{
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 __device__ __forceinline__ void wave_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -459,10 +468,10 @@ __device__ __forceinline__ void store_glf(ss_glf_t *dst, uint32_t ref16, const u
  * of elements with identical (q, strand), which leave every float sum
  * unchanged.
  * ------------------------------------------------------------------------ */
-#define GB 16               /* sites per group-kernel sub-group */
+#define GB 32               /* sites per group-kernel chunk (one fold lane per (site, sample)) */
 
 struct Slot3 {
-    uint32_t rec_n;      /* u32 index of the fold records | non-deleted depth << 16 */
+    uint32_t rec_n;      /* first record byte (17 bits) | non-deleted depth << 17 */
     uint32_t cnt01;      /* cnt[0] | cnt[1] << 16 */
     uint32_t cnt23;      /* cnt[2] | cnt[3] << 16 */
     uint32_t rms;        /* sum of min(mapQ & 0x7f, cap)^2 */
@@ -547,20 +556,18 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
     }
 }
 
-/* Fold of one (site, sample) by TWO lanes: role 0 accumulates esum, role 1
- * fsum (sniper_maqcns.c:165-172).  Both run the same instruction stream:
- *   acc = (float)((double)acc + fk[w] * m),  m = q (esum) or 1.0 (fsum),
- * and fk[w]*1.0 == fk[w] exactly, so each chain is bit-identical to the
- * reference's.  m is pulled out of the record with a lane-dependent bit-field
- * extract.  The two per-strand w counters live in one register (16-bit
- * fields, counting in units of 8 = the byte stride of fk), selected by the
- * record's strand<<4 field and saturated at w = 255 (:170).  Base groups are
- * walked longest first, so the wave-wide trip count is set by one long chain
- * per lane.
+/* Fold of one (site, sample) by one lane: esum and fsum (sniper_maqcns.c:
+ * 165-172) as two float accumulators fed double increments,
+ *   e = (float)((double)e + fk[w] * q),  f = (float)((double)f + fk[w]),
+ * in the reference's order, so each is bit-identical to the reference's.  The
+ * two per-strand w counters live in one register (16-bit fields, counting in
+ * units of 8 = the byte stride of fk), selected by the record's strand<<4
+ * field and saturated at w = 255 (:170).  Base groups are walked longest
+ * first, so the wave-wide trip count is set by one long chain per lane.
  *
  * The records lie in the wave's global buffer (L2): a chain is walked from
  * its top in blocks of 16 records, each block five dwords (one unaligned
- * 16-byte window) loaded one block ahead, four records per step through
+ * 16-byte window) loaded two blocks ahead, four records per step through
  * v_alignbyte as in the main kernel's fold.  A step past the chain's end
  * reads fk's zero entry (x + 0.0 == x). */
 #define GP_FK_ZERO 256
@@ -577,11 +584,9 @@ __device__ __forceinline__ void gp_block(const uint8_t *buf, int top, uint32_t (
 /* four steps of a chain from the window R of records k0 - 3 .. k0 (k0 in the
  * top byte); steps j >= m read fk's zero entry */
 template <bool TAIL>
-__device__ __forceinline__ void gp_steps(const char *fkb, uint32_t R, int m, uint32_t moff, uint32_t mwid,
-                                         uint32_t &W, float &e)
+__device__ __forceinline__ void gp_steps(const char *fkb, uint32_t R, int m, uint32_t &W, float &e, float &f)
 {
     double t[4];
-    uint32_t mq[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t r = R >> (24 - 8 * j);                      /* record k0 - j in the low byte */
@@ -591,32 +596,36 @@ __device__ __forceinline__ void gp_steps(const char *fkb, uint32_t R, int m, uin
         if (TAIL) w8 = j < m ? w8 : 8u * GP_FK_ZERO;
         W += 8u << sh;
         t[j] = *reinterpret_cast<const double *>(fkb + w8);
-        mq[j] = __builtin_amdgcn_ubfe(r, moff, mwid);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) e = (float)((double)e + t[j] * (double)mq[j]);
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t q = (R >> (24 - 8 * j)) & 63u;
+        e = (float)((double)e + t[j] * (double)q);
+        f = (float)((double)f + t[j]);
+    }
 }
 
 /* the 16 records below top in four steps (m: how many of them belong to the
  * chain); steps that no lane of the wave needs are skipped */
 template <bool TAIL>
 __device__ __forceinline__ void gp_block_steps(const char *fkb, const uint32_t (&w)[5], int top, int m,
-                                               uint32_t moff, uint32_t mwid, uint32_t &W, float &e)
+                                               uint32_t &W, float &e, float &f)
 {
     const uint32_t q = (uint32_t)(top - 16) & 3u;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         if (TAIL && !__ballot(m > 4 * s)) break;
-        gp_steps<TAIL>(fkb, __builtin_amdgcn_alignbyte(w[4 - s], w[3 - s], q), m - 4 * s, moff, mwid, W, e);
+        gp_steps<TAIL>(fkb, __builtin_amdgcn_alignbyte(w[4 - s], w[3 - s], q), m - 4 * s, W, e, f);
     }
 }
 
 /* chain of records [s0, s0 + n) of the buffer, from the top; w holds the
  * block below s0 + n (loaded by the caller) */
-__device__ __forceinline__ float gp_chain(const uint8_t *buf, uint32_t s0, uint32_t n, uint32_t (&w)[5],
-                                          const char *fkb, uint32_t moff, uint32_t mwid)
+__device__ __forceinline__ void gp_chain(const uint8_t *buf, uint32_t s0, uint32_t n, uint32_t (&w)[5],
+                                         const char *fkb, float &e, float &f)
 {
-    float e = 0.0f;
+    e = 0.0f;
+    f = 0.0f;
     uint32_t W = 0;
     if (__ballot(n >= 16u)) {
         /* whole blocks while any lane has 16 records left, the next two
@@ -629,10 +638,11 @@ __device__ __forceinline__ float gp_chain(const uint8_t *buf, uint32_t s0, uint3
             const int top = (int)(s0 + n) - (int)i;
             uint32_t wnn[5];
             gp_block(buf, max(top - 32, 0), wnn);
-            float e2 = e;
+            float e2 = e, f2 = f;
             uint32_t W2 = W;
-            gp_block_steps<false>(fkb, w, top, 16, moff, mwid, W2, e2);
+            gp_block_steps<false>(fkb, w, top, 16, W2, e2, f2);
             e = act ? e2 : e;
+            f = act ? f2 : f;
             W = act ? W2 : W;
 #pragma unroll
             for (int q = 0; q < 5; ++q) {
@@ -644,16 +654,14 @@ __device__ __forceinline__ float gp_chain(const uint8_t *buf, uint32_t s0, uint3
     /* the lane's last 0 .. 15 records (below its whole blocks): window w */
     const uint32_t m = n & 15u;
     if (__ballot(m > 0u)) {
-        if (m > 0u) gp_block_steps<true>(fkb, w, (int)(s0 + m), (int)m, moff, mwid, W, e);
+        if (m > 0u) gp_block_steps<true>(fkb, w, (int)(s0 + m), (int)m, W, e, f);
     }
-    return e;
 }
 
 __device__ __forceinline__ void fold_sample(const uint8_t *buf, uint32_t s0, const uint32_t cnt[4],
-                                            const double *fk, uint32_t role, float acc[4])
+                                            const double *fk, float es[4], float fs[4])
 {
     const uint32_t start1 = s0 + cnt[0], start2 = start1 + cnt[1], start3 = start2 + cnt[2];
-    const uint32_t moff = role ? 7u : 0u, mwid = role ? 1u : 6u;   /* fsum multiplier bit / q */
     const char *fkb = reinterpret_cast<const char *>(fk);
     uint32_t L = 0;
 #pragma unroll
@@ -672,10 +680,11 @@ __device__ __forceinline__ void fold_sample(const uint8_t *buf, uint32_t s0, con
     }
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) {
-        const float e = gp_chain(buf, sb[i], tb[i], w[i], fkb, moff, mwid);
+        float e, f;
+        gp_chain(buf, sb[i], tb[i], w[i], fkb, e, f);
 #pragma unroll
         for (uint32_t b2 = 0; b2 < 4; ++b2)
-            if (b2 == bb[i]) acc[b2] = e;
+            if (b2 == bb[i]) { es[b2] = e; fs[b2] = f; }
     }
 }
 
@@ -719,56 +728,36 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-/* Phases B, C, D for the G sites of a chunk.  Fold records are bytes of the
- * wave's global buffer `recs` (slot rec_n index). */
+/* Phases B, C, D for the G sites of a chunk: lane = slot (site * 2 + sample)
+ * folds, evaluates the ten genotypes and quantises its sample; lane = site
+ * decides.  Fold records are bytes of the wave's global buffer `recs` (slot
+ * rec_n index). */
 __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const uint8_t *recs,
                                            const Slot3 *slot, SlotRes *res, const uint32_t *sites,
                                            const uint32_t *refcs, const double *fk)
 {
-    /* opaque: the slot addresses are then formed here, not hoisted out of the
-     * kernel's loops (where they were live across the sort and spilled) */
-    uint32_t lane = lane_id();
-    asm volatile("" : "+v"(lane));
-    const int sl = (int)(lane >> 1);               /* slot = site * 2 + sample */
-    const uint32_t role = lane & 1u;               /* 0: esum lane, 1: fsum lane */
-    const bool act = sl < 2 * G;
-    float acc[4];
+    const uint32_t lane = lane_id_here();           /* slot addresses formed here */
+    const uint32_t sl = lane;
+    const bool act = sl < 2u * (uint32_t)G;
+    float es[4], fs[4];
     uint32_t cnt[4], depth = 0, rms = 0;
     if (act) {
         const Slot3 &m3 = slot[sl];
         cnt[0] = m3.cnt01 & 0xffffu; cnt[1] = m3.cnt01 >> 16;
         cnt[2] = m3.cnt23 & 0xffffu; cnt[3] = m3.cnt23 >> 16;
-        depth = m3.rec_n >> 16;
+        depth = m3.rec_n >> 17;
         rms = m3.rms;
-        fold_sample(recs, m3.rec_n & 0xffffu, cnt, fk, role, acc);
+        fold_sample(recs, m3.rec_n & 0x1ffffu, cnt, fk, es, fs);
     } else {
 #pragma unroll
-        for (int b = 0; b < 4; ++b) { acc[b] = 0.0f; cnt[b] = 0; }
+        for (int b = 0; b < 4; ++b) { es[b] = fs[b] = 0.0f; cnt[b] = 0; }
     }
-    wave_sync();
-    /* exchange esum / fsum within the lane pair (DPP, all lanes active) */
-    float es[4], fs[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const float o = __builtin_bit_cast(float, xor_lane<1>(__builtin_bit_cast(uint32_t, acc[b])));
-        es[b] = role ? o : acc[b];
-        fs[b] = role ? acc[b] : o;
-    }
-    /* likelihoods: role 0 evaluates genotypes 0..4, role 1 genotypes 5..9 */
     uint32_t c[4];
     const uint32_t tot = rescale_counts(cnt, c);
-    float mine[5];
-    geno_p5(role, es, fs, c, tot, a.m, mine);
-#pragma unroll
-    for (int t = 0; t < 5; ++t) mine[t] = act ? mine[t] : 0.0f;
     float p[10];
-#pragma unroll
-    for (int t = 0; t < 5; ++t) {
-        const float o = __builtin_bit_cast(float, xor_lane<1>(__builtin_bit_cast(uint32_t, mine[t])));
-        p[t] = role ? o : mine[t];
-        p[5 + t] = role ? mine[t] : o;
-    }
-    if (act && role == 0u) {
+    geno_p5(0u, es, fs, c, tot, a.m, p);
+    geno_p5(1u, es, fs, c, tot, a.m, p + 5);
+    if (act) {
         uint32_t lk[10], min_lk, rms_q, cns;
         glf_finish(p, es, depth, rms, a.m, lk, min_lk, rms_q, cns);
         SlotRes &r = res[sl];
@@ -779,9 +768,8 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
         r.cns = cns;
         r.depth = depth;
         if (a.glf) {
-            const uint32_t s = (uint32_t)sl >> 1;
-            store_glf(&a.glf[2ull * sites[s] + (sl & 1)], refcs[s] >> 8, lk, min_lk,
-                      rms_q, depth);
+            const uint32_t s = sl >> 1;
+            store_glf(&a.glf[2ull * sites[s] + (sl & 1u)], refcs[s] >> 8, lk, min_lk, rms_q, depth);
         }
     }
     wave_sync();
@@ -1506,7 +1494,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
     __syncthreads();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     /* the wave's fold records: a global (L2-resident) buffer that holds any
-     * chunk (16 sites x 2 x 2048 records), so a chunk's sites always fold
+     * chunk (32 sites x 2 x 2048 records), so a chunk's sites always fold
      * together; its address is re-derived where used (not held in SGPRs) */
     const size_t arena_off = (size_t)(blockIdx.x * GP_WAVES + wv) * SS_GRP_REC_BYTES + SS_GRP_REC_PAD;
     Slot3 *slot = L.slot[wv];
@@ -1517,10 +1505,8 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
     for (;;) {
-        /* opaque per chunk: the lane's LDS addresses are formed inside the
-         * loop, not hoisted out of it (where they stayed live and spilled) */
-        uint32_t lane = lane_id();
-        asm volatile("" : "+v"(lane));
+        /* per chunk: the lane's LDS addresses are formed inside the loop */
+        const uint32_t lane = lane_id_here();
         uint32_t ch = 0;
         if (lane == 0u) ch = atomicAdd(kernarg_args().wide_next, 1u);
         const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * GB;
@@ -1664,12 +1650,12 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
         }
         /* unit lanes publish their slot under the site's rank */
         const uint32_t us = lane >> 1;
-        const uint32_t rank_u = (uint32_t)__shfl((int)rank, (int)us);
+        const uint32_t rank_u = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(us << 2), (int)rank);
         const bool stay_u = is_u && ((staym >> us) & 1ull);
         if (stay_u) {
             Slot3 &st = slot[2u * rank_u + (lane & 1u)];
             const uint32_t ca = ucnt[lane][0], cb = ucnt[lane][1];
-            st.rec_n = L.u_base[wv][lane] | L.u_n[wv][lane] << 16;
+            st.rec_n = L.u_base[wv][lane] | L.u_n[wv][lane] << 17;
             st.cnt01 = (ca & 0xffffu) | (cb & 0xffffu) << 16;
             st.cnt23 = (ca >> 16) | (cb >> 16) << 16;
             st.rms = ucnt[lane][2];

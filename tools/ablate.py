@@ -47,21 +47,18 @@ EDITS = {
                 "    if (true) {\n#pragma unroll\n        for (int t = 0; t < 4; ++t) "
                 "x[t] = ((in.na + 4u * c + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;\n        return;\n    }\n"
                 "    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */\n")],
-    "gnosort": [("                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);\n                ln_levels<LN_R, 2>(v);\n",
-                 "                const LaneAcc acc = ln_keys(in, lut, nch, cap, v);\n")],
-    "gnomerge": [("                if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }\n"
-                  "                if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }\n"
-                  "                if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }\n"
-                  "                if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }\n", "")],
-    "gnorec": [("                        if (4 * i < lim) *reinterpret_cast<uint32_t *>(arena + ubase + 4u * (uint32_t)i) = "
-                "ln_rec_dword(v, i);\n", ""),
-               ("                        if (4 * i < lim)\n"
-                "                            *reinterpret_cast<uint4 *>(gbuf + ubase + 4u * (uint32_t)i) =\n"
-                "                                make_uint4(ln_rec_dword(v, i), ln_rec_dword(v, i + 1), ln_rec_dword(v, i + 2),\n"
-                "                                           ln_rec_dword(v, i + 3));\n", "")],
-    "gnofold": [("        if (in_lds) fold_sample(recs_lds, m3.rec_n & 0xffffu, cnt, fk, role, acc);\n"
-                 "        else fold_sample(recs_glb, m3.rec_n & 0xffffu, cnt, fk, role, acc);\n",
-                 "        for (int b = 0; b < 4; ++b) acc[b] = (float)cnt[b] + (float)recs_lds[b];\n")],
+    "gnosort": [("            ln_levels<LN_R, 2>(v);\n            if (__ballot(act && uU >= 2u))",
+                 "            if (__ballot(act && uU >= 2u))")],
+    "gnomerge": [("            if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }\n"
+                  "            if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }\n"
+                  "            if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }\n"
+                  "            if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }\n", "")],
+    "gnorec": [("                    *reinterpret_cast<uint4 *>(gbuf + ubase + 4u * (uint32_t)i) =\n"
+                "                        make_uint4(ln_rec_dword(v, i), ln_rec_dword(v, i + 1), ln_rec_dword(v, i + 2),\n"
+                "                                   ln_rec_dword(v, i + 3));\n",
+                "                    asm volatile(\"\" :: \"v\"(ubase));\n")],
+    "gnofold": [("        fold_sample(recs, m3.rec_n & 0x1ffffu, cnt, fk, es, fs);\n",
+                 "        for (int b = 0; b < 4; ++b) es[b] = fs[b] = (float)cnt[b] + (float)(m3.rec_n >> b);\n")],
     "gnofin": [("    geno_p5(role, es, fs, c, tot, a.m, mine);\n",
                 "    for (int t = 0; t < 5; ++t) mine[t] = es[t & 3] + (float)c[t & 3];\n")],
 }
