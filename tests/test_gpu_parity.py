@@ -116,6 +116,24 @@ def test_group_unit_boundaries(pkg, oracle, lt, ln, n, opts):
     assert_parity(pkg, oracle, batch, opts)
 
 
+@pytest.mark.parametrize("n_group", [1, 31, 32, 33, 95])
+@pytest.mark.parametrize("wild", [0.0, 0.002])
+def test_group_chunk_sizes(pkg, oracle, n_group, wild):
+    """The group kernel takes its listed sites 32 at a time (one chunk: the
+    records of all 32 fold together, one lane per (site, sample)): listed
+    counts below, at and just past a chunk, interleaved with main-kernel
+    sites so the listed order crosses main-wave segments; with wild reads a
+    chunk's sites leave for the deep kernel and the rest are compacted."""
+    deep = pkg.synth_batch_host(pkg.Synth.default(520, 480, **dict(EXOTIC, p_wild_qual=wild)), 5, n_group)
+    shallow = pkg.synth_batch_host(pkg.Synth.default(40, 30, **dict(EXOTIC, p_wild_qual=0.0)), 6, 3 * n_group + 50)
+    sites = []
+    for i in range(shallow.n_sites):
+        sites.append(shallow.site(i))
+        if i % 3 == 1 and i // 3 < deep.n_sites:
+            sites.append(deep.site(i // 3))
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), OPTSETS[0])
+
+
 @pytest.mark.parametrize("opts", OPTSETS)
 def test_kernel_routing_mix(pkg, oracle, opts):
     """One batch whose sites take every route: main kernel (<= 512 sort slots),
