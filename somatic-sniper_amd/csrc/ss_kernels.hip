@@ -19,8 +19,9 @@
  *     sample), with a read of minq >= 64 or malformed offsets are listed.
  *   ss_score_group  the listed sites with at most 2048 reads per sample: per
  *     (site, sample) a unit of 1..16 lanes sorts 128 keys per lane as above
- *     and merges across lanes (DPP); 16 sites are folded two lanes per
- *     (site, sample) and finished together.
+ *     and merges across lanes (DPP); the records go to a per-wave buffer
+ *     in HBM / L2, and a chunk of 32 sites is folded one lane per (site,
+ *     sample) and finished together; 12 waves per CU.
  *   ss_score_deep   one wave per site beyond that (any depth), with a wild
  *     read or malformed offsets: counting sort of the order-relevant key
  *     fields in LDS windows, then the same ordered fold, likelihood and
@@ -455,7 +456,7 @@ __device__ __forceinline__ void store_glf(ss_glf_t *dst, uint32_t ref16, const u
 /* --------------------------------------------------------------------------
  * Shared machinery of the lane-group kernel (sites past the main kernel's
  * per-lane network): 8-bit fold records, packed u16 min / max,
- * cross-lane exchanges, the two-lane ordered fold and the sub-group finish
+ * cross-lane exchanges, the one-lane ordered fold and the chunk finish
  * (likelihoods, quantisation, decision).
  *
  * 16-bit order key of a read (ln_chunk builds it):
@@ -1404,8 +1405,8 @@ void ss_score_main(ss_score_args a)
  * descending U, so every unit sits in one wave-sized batch of lanes and its
  * lanes are aligned; a batch merges up to its largest U (lanes of smaller
  * units sit the larger levels out).  The sorted contributing keys leave as
- * 8-bit fold records in the wave's arena, per unit in
- * ascending order, and finish_sub does the 16-site fold, likelihoods and
+ * 8-bit fold records in the wave's record buffer (HBM / L2), per unit in
+ * ascending order, and finish_sub does the 32-site fold, likelihoods and
  * decision.
  * ------------------------------------------------------------------------ */
 namespace {
