@@ -717,18 +717,6 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v)
     return v;
 }
 
-/* sum over the 64 lanes (no overflow: the caller's values are small), wave-uniform */
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false); /* row_shr:1 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false); /* row_shr:2 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false); /* row_shr:4 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false); /* row_shr:8 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); /* row_bcast:15 */
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); /* row_bcast:31 */
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
 /* Phases B, C, D for the G sites of a chunk: lane = slot (site * 2 + sample)
  * folds, evaluates the ten genotypes and quantises its sample; lane = site
  * decides.  Fold records are bytes of the wave's global buffer `recs` (slot
