@@ -723,7 +723,7 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v)
  * rec_n index). */
 __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const uint8_t *recs,
                                            const Slot3 *slot, SlotRes *res, const uint32_t *sites,
-                                           const uint32_t *refcs, const double *fk)
+                                           const uint32_t *refcs, const double *fk, const int16_t *qtab)
 {
     const uint32_t lane = lane_id_here();           /* slot addresses formed here */
     const uint32_t sl = lane;
@@ -763,7 +763,7 @@ __device__ __forceinline__ void finish_sub(const ss_score_args &a, int G, const 
     }
     wave_sync();
     /* the decision reads both samples' records straight from LDS */
-    if ((int)lane < G) decide_site(a, ss_tab_qadd(a.m), sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
+    if ((int)lane < G) decide_site(a, qtab, sites[lane], refcs[lane], res[2 * lane], res[2 * lane + 1]);
     wave_sync();
 }
 
@@ -1475,10 +1475,12 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
     __shared__ double fk[GP_FK_ZERO + 1];
     __shared__ uint2 lut[LN_LUT_BYTES / 8];
     __shared__ GroupLds L;
+    __shared__ int16_t qtab[1024];                  /* qAddTable, as in ss_score_main */
     const unsigned long long acc0 = *a.deep_acc;
     const uint32_t nsegs = min((uint32_t)(acc0 >> 32), a.deep_nseg), total = (uint32_t)acc0;
     if (nsegs == 0u) return;
     for (uint32_t i = threadIdx.x; i <= GP_FK_ZERO; i += blockDim.x) fk[i] = i < 256u ? ss_tab_fk(a.m)[i] : 0.0;
+    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) qtab[i] = (int16_t)ss_tab_qadd(a.m)[i];
     ln_lut_build(lut);
     __syncthreads();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1658,7 +1660,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
         /* the records' global stores complete before any lane reads them */
         __builtin_amdgcn_s_waitcnt(0x0f70);                  /* vmcnt(0) */
         wave_sync();
-        if (G2) finish_sub(kernarg_args(), (int)G2, kernarg_args().grp_rec + arena_off, slot, res, sites, refcs, fk);
+        if (G2) finish_sub(kernarg_args(), (int)G2, kernarg_args().grp_rec + arena_off, slot, res, sites, refcs, fk, qtab);
     }
 }
 
@@ -1825,7 +1827,9 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
 {
     __shared__ double fk[256];
     __shared__ DeepWave DW[DEEP_WAVES];
+    __shared__ int16_t qtab[1024];                  /* qAddTable, as in ss_score_main */
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) fk[i] = ss_tab_fk(a.m)[i];
+    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) qtab[i] = (int16_t)ss_tab_qadd(a.m)[i];
     __syncthreads();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     DeepWave &D = DW[wv];
@@ -1921,7 +1925,7 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
             if (k.glf) store_glf(&k.glf[2ull * s + smp], ref16, lk, min_lk, rms_q, r.depth);
         }
         wave_sync();
-        if (lane == 0u) decide_site(k, ss_tab_qadd(k.m), s, refc | ref16 << 8, D.res[0], D.res[1]);
+        if (lane == 0u) decide_site(k, qtab, s, refc | ref16 << 8, D.res[0], D.res[1]);
         wave_sync();
     }
 }
