@@ -213,7 +213,7 @@ static void write_batch(run_t *R, const batch_t *b, uint32_t ncalls)
 
 /* SS_TIMING=1: phase times on stderr (seconds since start) */
 static double t_start;
-static int timing;
+static int timing, debug_batches;
 static double now_s(void)
 {
     struct timespec ts;
@@ -249,6 +249,9 @@ static void *scorer_main(void *arg)
         pthread_mutex_unlock(&R->mu);
         const long ncalls = failed_get(R) ? -1 : score_batch(R, ctx, b);
         stamp("batch scored");
+        if (debug_batches)                                  /* SS_DEBUG_BATCHES=1: one line per scored batch */
+            fprintf(stderr, "[batch] run %p scorer %d seq %llu sites %zu first %u:%u calls %ld\n", (void *)R, k,
+                    (unsigned long long)s, b->n, b->n ? b->tid[0] : 0u, b->n ? b->pos[0] : 0u, ncalls);
         pthread_mutex_lock(&R->mu);
         while (R->seq_write != s) pthread_cond_wait(&R->cv, &R->mu);   /* output in batch order */
         pthread_mutex_unlock(&R->mu);
@@ -599,6 +602,7 @@ int main(int argc, char *argv[])
 {
     t_start = now_s();
     timing = getenv("SS_TIMING") != NULL;
+    debug_batches = getenv("SS_DEBUG_BATCHES") != NULL;
     ss_params_t prm;
     ss_params_default(&prm);
     const char *normal_id = "NORMAL", *tumor_id = "TUMOR", *fn_fa = NULL, *fmt_name = "classic";

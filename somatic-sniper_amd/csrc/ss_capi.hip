@@ -11,11 +11,13 @@
  * Contexts are independent (include/sniper_amd.h): nothing here waits for
  * the whole device.  A context waits only for its own work -- its `done`
  * event (the latest launch, whatever stream it went to) and its own stream
- * -- and allocates and frees its device memory stream-ordered
- * (hipMallocAsync / hipFreeAsync), because hipFree and hipHostFree imply a
- * hipDeviceSynchronize that would make one context wait for another's
- * kernels.  Page-locked staging memory is malloc'd and registered
- * (hipHostRegister / hipHostUnregister) for the same reason.
+ * -- for its launches and copies.  Its device memory comes from hipMalloc /
+ * hipFree (see dev_alloc: the stream-ordered pool misbehaved under
+ * concurrent context creation); allocations happen at creation and when a
+ * work list or staging area grows, so hipFree's device-wide wait is rare.
+ * Page-locked staging memory is malloc'd and registered (hipHostRegister /
+ * hipHostUnregister) instead of hipHostMalloc / hipHostFree, whose free
+ * would wait for the whole device.
  */
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -86,15 +88,28 @@ extern "C" const char *ss_strerror(int code)
 
 /* stream-ordered device allocation: usable on any stream once `s` has
  * reached it (callers order their use after it) */
+/* Device memory: hipMalloc / hipFree, not the stream-ordered pool.  With
+ * several contexts of one process allocating from the device's default pool
+ * on their own streams at once (the CLI's contig groups x scorers), a context
+ * intermittently got a table allocation whose contents ended up wrong (its
+ * batches emitted nothing; tools/repro_groups.py: 4-5 runs in 25 with
+ * hipMallocAsync, 1 in 30 with the async calls serialized by a mutex, 0 in 25
+ * with hipMalloc).  Allocations happen at context creation and when a
+ * work list or staging area grows, so the device-wide wait of hipFree is rare. */
 static int dev_alloc(void **p, size_t bytes, hipStream_t s)
 {
-    if (hipMallocAsync(p, bytes ? bytes : 16, s) != hipSuccess) { *p = nullptr; return SS_E_NOMEM; }
+    (void)s;
+    if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) { *p = nullptr; return SS_E_NOMEM; }
     return SS_OK;
 }
 
+/* the buffer's pending work on s completes first (hipFree also waits for the device) */
 static void dev_free(void *&p, hipStream_t s)
 {
-    if (p) hipFreeAsync(p, s);
+    if (p) {
+        hipStreamSynchronize(s);
+        hipFree(p);
+    }
     p = nullptr;
 }
 
