@@ -289,6 +289,30 @@ def test_contig_groups_output_matches_reference(datasets, tmp_path):
 @pytest.mark.gpu
 @need_native
 @need_ref
+@need_index
+def test_contig_groups_concurrent_contexts_repeated(datasets, tmp_path):
+    """2 contig ranges x 2 scorers on one device: four contexts created at the
+    same moment on four threads.  With stream-ordered device allocation about
+    one run in five lost a batch's calls (DESIGN.md §2, tools/repro_groups.py);
+    every one of 10 runs must equal the reference CLI."""
+    strip = lambda s: "".join(l for l in s.splitlines(True) if not l.startswith("##fileDate"))
+    d, fa, t, n = datasets[2]                   # bamgen seed 2, 60x/30x, 4 contigs
+    dst = tmp_path / "rep"
+    assert _indexed_copy(d, fa, t, n, dst)
+    args = ["-F", "vcf", "-Q", "0", "-f", fa, t, n]
+    pr = _run([REF_CLI] + args + ["ref_rep.out"], d)
+    assert pr.returncode == 0, pr.stderr
+    ref = strip(open(os.path.join(d, "ref_rep.out")).read())
+    env = {"SS_CONTIG_GROUPS": "2", "SS_DEVICES": "0,0", "SS_DEVICES_SHARED": "1"}
+    for r in range(10):
+        pn = _run([NATIVE] + args + ["nat_rep.out"], str(dst), env)
+        assert pn.returncode == 0, pn.stderr
+        assert strip((dst / "nat_rep.out").read_text()) == ref, f"run {r}"
+
+
+@pytest.mark.gpu
+@need_native
+@need_ref
 def test_multi_scorer_output_identical(datasets):
     """SS_DEVICES with several scorers (all on the box's one GPU here; one
     per device on a multi-GPU node) and small batches, so consecutive batches
