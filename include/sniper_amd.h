@@ -169,7 +169,9 @@ void ss_ctx_destroy(ss_ctx_t *ctx);
  * other: a launch on another stream than the previous one (or the host path's
  * own stream) first waits for the previous launch on the device.  Use one
  * context per stream for concurrent batches.  No depth limit: sites of any
- * depth are scored. */
+ * depth are scored.  A batch with more sites than any before it on this
+ * context grows the context's work lists first (hipFree + hipMalloc: that
+ * call waits for the device), so size the first batch like the largest. */
 int  ss_score_batch_device(ss_ctx_t *ctx, const ss_batch_t *batch,
                            const ss_out_t *out, void *stream);
 
