@@ -231,7 +231,8 @@ def live_counters(args, kernel="ss_score_main"):
         try:
             cmd = [exe, "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "run", "--",
                    sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
-                   "--c4-scale", str(args.c4_scale), "--chunk", str(args.chunk), "--sites", str(args.sites),
+                   *(["--c4-scale", str(args.c4_scale)] if args.c4_scale is not None else []),
+                   "--chunk", str(args.chunk), "--sites", str(args.sites),
                    "--lt", str(args.lt), "--ln", str(args.ln), "--seed", str(args.seed),
                    "--pmc-launches", str(args.pmc_launches), "--pmc-batches", str(args.pmc_batches)]
             # own process group: a pass that overruns is killed with its python child
