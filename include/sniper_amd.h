@@ -42,9 +42,12 @@ extern "C" {
 #define SS_E_INVAL      -1   /* bad argument / malformed batch               */
 #define SS_E_HIP        -2   /* a HIP runtime call failed                     */
 #define SS_E_NOMEM      -3   /* host or device allocation failed             */
-#define SS_E_TABLES     -4   /* host tables differ from the pinned reference  */
+#define SS_E_TABLES     -4   /* host tables differ from the pinned reference,
+                                or the device copy no longer matches them     */
 #define SS_E_CAPACITY   -5   /* emitted-call buffer overflowed (n_calls > cap)*/
 #define SS_E_NODEV      -6   /* no HIP device / device index out of range     */
+#define SS_E_CORRUPT    -7   /* debug build: a device buffer's guard band was
+                                overwritten (make -C somatic-sniper_amd debug) */
 
 /* ---- packed pileup read ---------------------------------------------------
  * One u32 per NON-DELETED pileup read (bam_pileup1_t with is_del==0 and the
@@ -170,15 +173,20 @@ void ss_ctx_destroy(ss_ctx_t *ctx);
  * own stream) first waits for the previous launch on the device.  Use one
  * context per stream for concurrent batches.  No depth limit: sites of any
  * depth are scored.  A batch with more sites than any before it on this
- * context grows the context's work lists first (hipFree + hipMalloc: that
- * call waits for the device), so size the first batch like the largest. */
+ * context grows the context's work lists first (a new device block; the
+ * outgrown one is kept until ss_ctx_destroy): no call here synchronizes the
+ * host with the device. */
 int  ss_score_batch_device(ss_ctx_t *ctx, const ss_batch_t *batch,
                            const ss_out_t *out, void *stream);
 
 /* Wait for the context's outstanding work and report sticky device-side
  * errors: SS_E_INVAL if a batch had malformed read offsets (a site whose
  * offsets decrease or pass off[n_sites]: it scores -2 and no read is loaded
- * for it).  Clears the sticky bits. */
+ * for it).  Clears the sticky bits.  Also re-verifies the context's device
+ * tables against the host's (a fingerprint kernel; SS_E_TABLES if they no
+ * longer match, as ss_ctx_create checks after the upload), and in the debug
+ * build the guard bands around every device buffer (SS_E_CORRUPT).
+ * ss_score_batch_host runs this after every batch. */
 int  ss_ctx_check(ss_ctx_t *ctx);
 
 /* Score a host batch: stages through pinned buffers, H2D, kernel, D2H, sorts

@@ -40,6 +40,7 @@ __all__ = [
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 SS_OK, SS_E_INVAL, SS_E_HIP, SS_E_NOMEM, SS_E_TABLES, SS_E_CAPACITY, SS_E_NODEV = 0, -1, -2, -3, -4, -5, -6
+SS_E_CORRUPT = -7
 
 # every symbol include/sniper_amd.h declares
 EXPORTED_SYMBOLS = (
@@ -244,6 +245,8 @@ def load_library():
         lib.ss_model_last_source.restype = C.c_int
     lib.ss_kernel_time_log.argtypes = [vp, vp, C.c_int]
     lib.ss_kernel_time_log_k.argtypes = [vp, C.c_int, vp, C.c_int]
+    if hasattr(lib, "ss__test_poke_table"):         # test hook, not in the public header
+        lib.ss__test_poke_table.argtypes = [vp, u64, C.c_int]
     if lib.ss_abi_version() != 1:
         raise RuntimeError("libsniper_amd.so ABI mismatch")
     _LIB = lib
@@ -389,6 +392,10 @@ class Context:
 
     def check(self):
         _check(self.lib.ss_ctx_check(self.h), "device work")
+
+    def _poke_table(self, byte_offset: int, value: int):
+        """Test hook: overwrite one byte of the device tables (ss_ctx_check must then fail)."""
+        _check(self.lib.ss__test_poke_table(self.h, byte_offset, value), "ss__test_poke_table")
 
     def set_kernel_timing(self, enable: bool):
         _check(self.lib.ss_set_kernel_timing(self.h, 1 if enable else 0), "ss_set_kernel_timing")

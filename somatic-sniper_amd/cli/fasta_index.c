@@ -72,7 +72,17 @@ static const fai_entry_t *find(const fasta_index_t *fi, const char *name)
 }
 
 /* Scan the FASTA once, recording per sequence its base count, the offset of
- * its first base and its line geometry (the rules of samtools fai_build). */
+ * its first base and its line geometry.
+ *
+ * This is a close restatement of samtools 0.1.6 fai_build_core
+ * (samtools-0.1.6/faidx.c:59-129, vendored in the reference as
+ * vendor/samtools-0.1.6.tar.gz): the same line-state machine (state 0/1/2/3,
+ * the l1/l2-style line_blen/line_len bookkeeping), the same branch order and
+ * the same error messages.  It is kept that close on purpose: the .fai bytes
+ * the reference writes next to the FASTA and its stderr on malformed input
+ * are part of the CLI's parity contract (tests/test_cli_native.py compares
+ * both).  The I/O (stdio instead of RAZF) and the name table are this file's
+ * own. */
 static int build_index(fasta_index_t *fi, FILE *fp, const char *fn)
 {
     char *name = NULL;

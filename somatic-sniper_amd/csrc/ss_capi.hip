@@ -11,20 +11,25 @@
  * Contexts are independent (include/sniper_amd.h): nothing here waits for
  * the whole device.  A context waits only for its own work -- its `done`
  * event (the latest launch, whatever stream it went to) and its own stream
- * -- for its launches and copies.  Its device memory comes from hipMalloc /
- * hipFree (see dev_alloc: the stream-ordered pool misbehaved under
- * concurrent context creation); allocations happen at creation and when a
- * work list or staging area grows, so hipFree's device-wide wait is rare.
- * Page-locked staging memory is malloc'd and registered (hipHostRegister /
- * hipHostUnregister) instead of hipHostMalloc / hipHostFree, whose free
- * would wait for the whole device.
+ * -- for its launches and copies.  Device memory comes from hipMalloc through
+ * a per-device cache of idle blocks (dev_alloc below): nothing is handed back
+ * to HIP (hipFree waits for the whole device) while another context of the
+ * process lives on that device.  Page-locked staging memory is malloc'd and
+ * registered (hipHostRegister / hipHostUnregister) instead of hipHostMalloc /
+ * hipHostFree, whose free would wait for the whole device.
+ *
+ * Every context verifies its device tables after the upload and in each
+ * ss_ctx_check (a fingerprint kernel against the host's sums), so tables that
+ * stop holding what was uploaded are reported (SS_E_TABLES), never scored.
  */
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -35,6 +40,8 @@
 
 #define SS_EV_PER_LAUNCH 4   /* before main, after main, after wide, after deep */
 
+struct dev_blk;
+
 struct ss_ctx {
     int device;
     int n_cu;
@@ -43,7 +50,8 @@ struct ss_ctx {
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
     uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6..7] listed
-                                 entries | segments << 32, [8] the group kernel's chunk counter */
+                                 entries | segments << 32, [8] the group kernel's chunk counter,
+                                 [16..21] the table fingerprint (3 x u64) */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
     uint32_t *d_deep_seg;     /* listed segments' first entries, then their main-wave ids */
@@ -63,7 +71,13 @@ struct ss_ctx {
     uint32_t *d_cdf;                        /* [2][SS_SYNTH_MAXCDF] */
     void *d_scan_tmp; size_t scan_tmp_sz;
     uint32_t *d_depth_tmp; size_t depth_tmp_n;
+    /* device memory (dev_alloc): blocks in use, blocks outgrown but possibly still read */
+    std::vector<dev_blk> *blocks, *retired;
+    uint64_t fp_expect[3];    /* host fingerprint of the uploaded tables: coef, lhet, the rest */
+    int counted;              /* included in g_live */
 };
+
+#define SS_NCOUNTERS 32
 
 #define HIPCHK(x)                                   \
     do {                                            \
@@ -79,38 +93,148 @@ extern "C" const char *ss_strerror(int code)
     case SS_E_INVAL: return "invalid argument or malformed batch";
     case SS_E_HIP: return "HIP runtime error";
     case SS_E_NOMEM: return "out of memory";
-    case SS_E_TABLES: return "host model tables differ from the reference (libm mismatch)";
+    case SS_E_TABLES: return "model tables differ from the reference (libm mismatch), or the device copy no longer matches the host's";
     case SS_E_CAPACITY: return "capacity exceeded (emitted calls, work lists or pileup depth)";
     case SS_E_NODEV: return "no usable HIP device";
+    case SS_E_CORRUPT: return "device memory outside a buffer was overwritten (debug guard bands)";
     default: return "unknown error";
     }
 }
 
-/* stream-ordered device allocation: usable on any stream once `s` has
- * reached it (callers order their use after it) */
-/* Device memory: hipMalloc / hipFree, not the stream-ordered pool.  With
- * several contexts of one process allocating from the device's default pool
- * on their own streams at once (the CLI's contig groups x scorers), a context
- * intermittently got a table allocation whose contents ended up wrong (its
- * batches emitted nothing; tools/repro_groups.py: 4-5 runs in 25 with
- * hipMallocAsync, 1 in 30 with the async calls serialized by a mutex, 0 in 25
- * with hipMalloc).  Allocations happen at context creation and when a
- * work list or staging area grows, so the device-wide wait of hipFree is rare. */
-static int dev_alloc(void **p, size_t bytes, hipStream_t s)
+/* ---- device memory ---------------------------------------------------------
+ * Blocks come from hipMalloc and go back to HIP (hipFree, which waits for the
+ * whole device) only when the last context of the process on their device is
+ * destroyed.  Until then a block a context no longer needs -- a work list or
+ * staging area it outgrew, or everything it held at ss_ctx_destroy -- goes to
+ * a per-device cache of idle blocks that later allocations of any context
+ * reuse.  So neither a scoring call nor one context's teardown waits for
+ * another context's kernels (test_contexts_do_not_wait_for_each_other).
+ *
+ * A block enters the idle cache only when the device is done with it: at
+ * ss_ctx_destroy after the context's own work has completed (ctx_quiesce);
+ * a staging area after its stream was synchronized; a work list that grew
+ * while launches may still read it stays on the context's retired list until
+ * ss_ctx_destroy.
+ *
+ * Round 4 took device memory from the stream-ordered pool (hipMallocAsync /
+ * hipFreeAsync); contexts created while other contexts of the process were
+ * being destroyed then lost batches (tools/pool_race.hip
+ * reproduces it without any kernel of ours).
+ *
+ * Debug build (make debug, -DSS_DEBUG_CANARY): every block carries guard bands
+ * of SS_GUARD bytes before and after it, filled with 0xA5 at allocation and
+ * checked by ss_ctx_check and ss_ctx_destroy (SS_E_CORRUPT on a difference). */
+#ifdef SS_DEBUG_CANARY
+#define SS_GUARD ((size_t)4096)
+#else
+#define SS_GUARD ((size_t)0)
+#endif
+
+struct dev_blk {
+    void *base;       /* hipMalloc'd address; the user pointer is base + SS_GUARD */
+    size_t bytes;     /* usable bytes */
+    int device;
+};
+
+static std::mutex g_mem_mu;
+static std::vector<dev_blk> g_idle;          /* blocks no context uses, any device */
+static std::vector<int> g_live;              /* live contexts per device */
+
+static inline void *blk_user(const dev_blk &b) { return (char *)b.base + SS_GUARD; }
+
+static int guards_fill(const dev_blk &b, hipStream_t s)
 {
-    (void)s;
-    if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) { *p = nullptr; return SS_E_NOMEM; }
+#ifdef SS_DEBUG_CANARY
+    if (hipMemsetAsync(b.base, 0xA5, SS_GUARD, s) != hipSuccess ||
+        hipMemsetAsync((char *)blk_user(b) + b.bytes, 0xA5, SS_GUARD, s) != hipSuccess)
+        return SS_E_HIP;
+#else
+    (void)b; (void)s;
+#endif
     return SS_OK;
 }
 
-/* the buffer's pending work on s completes first (hipFree also waits for the device) */
-static void dev_free(void *&p, hipStream_t s)
+/* a block of >= bytes on c's device: an idle one of at most twice the size,
+ * else a new hipMalloc.  Recorded in c->blocks. */
+static int dev_alloc(ss_ctx_t *c, void **p, size_t bytes, hipStream_t s)
 {
-    if (p) {
-        hipStreamSynchronize(s);
-        hipFree(p);
+    const size_t need = (std::max<size_t>(bytes, 16) + 255) & ~(size_t)255;
+    dev_blk b = {nullptr, 0, c->device};
+    *p = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_mem_mu);
+        size_t best = g_idle.size();
+        for (size_t i = 0; i < g_idle.size(); ++i) {
+            const dev_blk &x = g_idle[i];
+            if (x.device == c->device && x.bytes >= need && x.bytes / 2 <= need &&
+                (best == g_idle.size() || x.bytes < g_idle[best].bytes))
+                best = i;
+        }
+        if (best < g_idle.size()) {
+            b = g_idle[best];
+            g_idle[best] = g_idle.back();
+            g_idle.pop_back();
+        }
     }
+    if (!b.base) {
+        if (hipSetDevice(c->device) != hipSuccess) return SS_E_HIP;
+        if (hipMalloc(&b.base, need + 2 * SS_GUARD) != hipSuccess) {
+            (void)hipGetLastError();
+            return SS_E_NOMEM;
+        }
+        b.bytes = need;
+    }
+    c->blocks->push_back(b);
+    *p = blk_user(b);
+    return guards_fill(b, s);
+}
+
+/* p is no longer used by c; `idle_now`: the device is done with it (else it
+ * stays on c's retired list until ss_ctx_destroy) */
+static void dev_release(ss_ctx_t *c, void *&p, bool idle_now)
+{
+    if (!p) return;
+    auto &v = *c->blocks;
+    for (size_t i = 0; i < v.size(); ++i)
+        if (blk_user(v[i]) == p) {
+            const dev_blk b = v[i];
+            v[i] = v.back();
+            v.pop_back();
+            if (idle_now) {
+                std::lock_guard<std::mutex> g(g_mem_mu);
+                g_idle.push_back(b);
+            } else {
+                c->retired->push_back(b);
+            }
+            break;
+        }
     p = nullptr;
+}
+
+/* debug build: SS_E_CORRUPT if a guard band of one of c's blocks changed */
+static int guards_check(ss_ctx_t *c)
+{
+#ifdef SS_DEBUG_CANARY
+    std::vector<unsigned char> h(2 * SS_GUARD);
+    for (auto *list : {c->blocks, c->retired})
+        for (const dev_blk &b : *list) {
+            if (hipMemcpyAsync(h.data(), b.base, SS_GUARD, hipMemcpyDeviceToHost, c->hstream) != hipSuccess ||
+                hipMemcpyAsync(h.data() + SS_GUARD, (char *)blk_user(b) + b.bytes, SS_GUARD, hipMemcpyDeviceToHost,
+                               c->hstream) != hipSuccess ||
+                hipStreamSynchronize(c->hstream) != hipSuccess)
+                return SS_E_HIP;
+            for (size_t i = 0; i < h.size(); ++i)
+                if (h[i] != 0xA5) {
+                    fprintf(stderr, "[sniper_amd] guard band of device block %p (%zu bytes) overwritten at %s%zu\n",
+                            blk_user(b), b.bytes, i < SS_GUARD ? "-" : "+",
+                            i < SS_GUARD ? SS_GUARD - i : i - SS_GUARD);
+                    return SS_E_CORRUPT;
+                }
+        }
+#else
+    (void)c;
+#endif
+    return SS_OK;
 }
 
 /* page-locked host memory without hipHostMalloc / hipHostFree (the free
@@ -142,18 +266,53 @@ static void ctx_quiesce(ss_ctx_t *c)
     if (c->hstream) hipStreamSynchronize(c->hstream);
 }
 
+/* fingerprint the context's device tables (ss_tab_fingerprint) and compare
+ * with the host's sums; the caller's stream order puts this after the upload /
+ * the launches it wants checked.  Synchronizes the context's stream. */
+static int tables_verify(ss_ctx_t *c)
+{
+    unsigned long long fp[3] = {0, 0, 0};
+    hipStream_t hs = c->hstream;
+    unsigned long long *dfp = reinterpret_cast<unsigned long long *>(c->d_counters + 16);
+    HIPCHK(hipMemsetAsync(dfp, 0, sizeof fp, hs));
+    if (ss_launch_tab_fingerprint(c->d_tab, dfp, hs) != 0) return SS_E_HIP;
+    HIPCHK(hipMemcpyAsync(fp, dfp, sizeof fp, hipMemcpyDeviceToHost, hs));
+    HIPCHK(hipStreamSynchronize(hs));
+    if (fp[0] == c->fp_expect[0] && fp[1] == c->fp_expect[1] && fp[2] == c->fp_expect[2]) return SS_OK;
+    fprintf(stderr, "[sniper_amd] device %d: the context's device tables no longer match the host's (%s%s%s differ)\n",
+            c->device, fp[0] != c->fp_expect[0] ? "coef " : "", fp[1] != c->fp_expect[1] ? "lhet " : "",
+            fp[2] != c->fp_expect[2] ? "fk/qAdd/prior/nt16" : "");
+    return SS_E_TABLES;
+}
+
 extern "C" void ss_ctx_destroy(ss_ctx_t *c)
 {
     if (!c) return;
     hipSetDevice(c->device);
     ctx_quiesce(c);
-    if (c->hstream) {
-        void **ptrs[] = {(void **)&c->d_tab, (void **)&c->d_counters, (void **)&c->d_deep_list,
-                         (void **)&c->d_deep_seg, &c->d_stage, (void **)&c->d_cdf, &c->d_scan_tmp,
-                         (void **)&c->d_depth_tmp, (void **)&c->d_grp_rec};
-        for (void **p : ptrs) dev_free(*p, c->hstream);
-        hipStreamSynchronize(c->hstream);
+    if (c->blocks && c->hstream && guards_check(c) != SS_OK)
+        fprintf(stderr, "[sniper_amd] ss_ctx_destroy: device memory corrupted (see above)\n");
+    /* the context's work has completed: its blocks are idle now */
+    std::vector<dev_blk> trim;
+    if (c->blocks) {
+        std::lock_guard<std::mutex> g(g_mem_mu);
+        for (auto *list : {c->blocks, c->retired})
+            for (const dev_blk &b : *list) g_idle.push_back(b);
+        if ((size_t)c->device < g_live.size() && c->counted && --g_live[c->device] == 0) {
+            /* the process's last context on this device: hand its idle blocks back to HIP */
+            for (size_t i = 0; i < g_idle.size();)
+                if (g_idle[i].device == c->device) {
+                    trim.push_back(g_idle[i]);
+                    g_idle[i] = g_idle.back();
+                    g_idle.pop_back();
+                } else {
+                    ++i;
+                }
+        }
     }
+    for (const dev_blk &b : trim) hipFree(b.base);
+    delete c->blocks;
+    delete c->retired;
     pinned_free(c->h_stage);
     if (c->ev) {
         for (hipEvent_t e : *c->ev) hipEventDestroy(e);
@@ -176,7 +335,15 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
     if (!c) return SS_E_NOMEM;
     c->device = device;
     c->ev = new std::vector<hipEvent_t>();
-    if ((rc = ss_host_model_build(p, &c->hm)) != SS_OK) { delete c->ev; free(c); return rc; }
+    c->blocks = new std::vector<dev_blk>();
+    c->retired = new std::vector<dev_blk>();
+    {
+        std::lock_guard<std::mutex> g(g_mem_mu);
+        if (g_live.size() < (size_t)ndev) g_live.resize(ndev, 0);
+        ++g_live[device];
+        c->counted = 1;
+    }
+    if ((rc = ss_host_model_build(p, &c->hm)) != SS_OK) { ss_ctx_destroy(c); return rc; }
     if (hipSetDevice(device) != hipSuccess) { ss_ctx_destroy(c); return SS_E_HIP; }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { ss_ctx_destroy(c); return SS_E_HIP; }
@@ -188,7 +355,7 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
     }
     hipStream_t hs = c->hstream;
 #define TRY(x) do { if ((rc = (x)) != SS_OK) { ss_ctx_destroy(c); return rc; } } while (0)
-    TRY(dev_alloc((void **)&c->d_tab, SS_TAB_BYTES, hs));
+    TRY(dev_alloc(c, (void **)&c->d_tab, SS_TAB_BYTES, hs));
     {
         struct { size_t off; const void *src; size_t n; } parts[] = {
             {SS_TAB_COEF, c->hm.coef, ((size_t)64 << 16) * sizeof(double)},
@@ -204,18 +371,32 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
                 ss_ctx_destroy(c);
                 return SS_E_HIP;
             }
+        /* the host's fingerprint of the same image: coef and lhet from the
+         * process-wide table entry, the rest assembled here */
+        static_assert(SS_TAB_COEF / 8 == SS_FP_COEF_WORD && SS_TAB_LHET / 8 == SS_FP_LHET_WORD, "fingerprint layout");
+        std::vector<uint8_t> rest(SS_TAB_BYTES - SS_TAB_FK);
+        for (auto &pt : parts)
+            if (pt.off >= SS_TAB_FK) memcpy(rest.data() + (pt.off - SS_TAB_FK), pt.src, pt.n);
+        c->fp_expect[0] = c->hm.fp_coef;
+        c->fp_expect[1] = c->hm.fp_lhet;
+        c->fp_expect[2] = ss_tab_fp_words(rest.data(), rest.size() / 8, SS_TAB_FK / 8);
+        /* `rest` is pageable and local: the copies above read other buffers */
     }
-    TRY(dev_alloc((void **)&c->d_counters, 16 * sizeof(uint32_t), hs));
-    TRY(dev_alloc((void **)&c->d_deep_seg, 2 * (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t), hs));
-    TRY(dev_alloc((void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t), hs));
+    TRY(dev_alloc(c, (void **)&c->d_counters, SS_NCOUNTERS * sizeof(uint32_t), hs));
+    TRY(dev_alloc(c, (void **)&c->d_deep_seg, 2 * (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t), hs));
+    TRY(dev_alloc(c, (void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t), hs));
     /* one group-kernel workgroup per CU (wide_grid below), one buffer per wave */
-    TRY(dev_alloc((void **)&c->d_grp_rec, (size_t)c->n_cu * (SS_WIDE_BLOCK / 64) * SS_GRP_REC_BYTES, hs));
+    TRY(dev_alloc(c, (void **)&c->d_grp_rec, (size_t)c->n_cu * (SS_WIDE_BLOCK / 64) * SS_GRP_REC_BYTES, hs));
 #undef TRY
-    /* the tables, lists and counters are complete before any launch can use them */
-    if (hipMemsetAsync(c->d_counters, 0, 16 * sizeof(uint32_t), hs) != hipSuccess ||
-        hipStreamSynchronize(hs) != hipSuccess) {
+    /* the tables, lists and counters are complete before any launch can use
+     * them, and the tables read back as uploaded */
+    if (hipMemsetAsync(c->d_counters, 0, SS_NCOUNTERS * sizeof(uint32_t), hs) != hipSuccess) {
         ss_ctx_destroy(c);
         return SS_E_HIP;
+    }
+    if ((rc = tables_verify(c)) != SS_OK || (rc = guards_check(c)) != SS_OK) {
+        ss_ctx_destroy(c);
+        return rc;
     }
     *out = c;
     return SS_OK;
@@ -247,16 +428,20 @@ extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double
 
 /* the deep list buffer holds two lists of deep_cap entries: the main
  * kernel's per-wave segments (deep) and the group kernel's overflow (deep2).
- * Grown on the launch stream `s`, which has already waited for the
- * context's previous launch (the last user of the old list). */
+ * Grown for a batch larger than any before (by at least half, so a run of
+ * growing batches allocates O(log) times); the old list may still be read by
+ * the context's previous launch, so it is retired, not reused, until
+ * ss_ctx_destroy.  No host or device synchronization. */
 static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
 {
     if (n_sites <= c->deep_cap) return SS_OK;
     uint64_t cap = std::max<uint64_t>(n_sites, 1u << 16);
-    if (cap > 0xffffffffull) return SS_E_INVAL;
-    dev_free(*(void **)&c->d_deep_list, s);
+    if (c->deep_cap) cap = std::max<uint64_t>(cap, (uint64_t)c->deep_cap + c->deep_cap / 2);
+    cap = std::min<uint64_t>(cap, 0xffffffffull);
+    if (cap < n_sites) return SS_E_INVAL;
+    dev_release(c, *(void **)&c->d_deep_list, false);
     c->deep_cap = 0;
-    if (dev_alloc((void **)&c->d_deep_list, 2 * cap * sizeof(uint32_t), s)) return SS_E_NOMEM;
+    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 2 * cap * sizeof(uint32_t), s)) return rc;
     c->deep_cap = (uint32_t)cap;
     return SS_OK;
 }
@@ -388,21 +573,43 @@ extern "C" int ss_kernel_time_log(ss_ctx_t *c, double *ms, int cap)
 }
 
 /* waits for this context's own work (its latest launch, its stream), not
- * for other contexts' or the caller's other work on the device */
+ * for other contexts' or the caller's other work on the device; then checks
+ * that the device tables still hold what was uploaded (SS_E_TABLES) and, in
+ * the debug build, the guard bands (SS_E_CORRUPT) */
 extern "C" int ss_ctx_check(ss_ctx_t *c)
 {
     uint32_t err = 0;
+    int rc;
     if (!c) return SS_E_INVAL;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t hs = c->hstream;
     if (c->launched) HIPCHK(hipStreamWaitEvent(hs, c->done, 0));
     HIPCHK(hipMemcpyAsync(&err, c->d_counters + 2, sizeof(err), hipMemcpyDeviceToHost, hs));
-    HIPCHK(hipStreamSynchronize(hs));
+    if ((rc = tables_verify(c)) != SS_OK) return rc;       /* synchronizes hs */
+    if ((rc = guards_check(c)) != SS_OK) return rc;
     if (err) {
         HIPCHK(hipMemsetAsync(c->d_counters + 2, 0, sizeof(uint32_t), hs));
         HIPCHK(hipStreamSynchronize(hs));
         return (err & SS_KERR_MALFORMED) ? SS_E_INVAL : SS_E_CAPACITY;
     }
+    return SS_OK;
+}
+
+/* test hook (not in the public header): overwrite one byte of the context's
+ * device tables, so the tests can see ss_ctx_check report it */
+extern "C" int ss__test_poke_table(ss_ctx_t *c, uint64_t byte_offset, int value)
+{
+    /* the debug build maps offsets SS_TAB_BYTES .. +15 to the first bytes of
+     * the guard band after the table block */
+    if (!c || byte_offset >= SS_TAB_BYTES + (SS_GUARD ? 16 : 0)) return SS_E_INVAL;
+    uint8_t *dst = c->d_tab + byte_offset;
+    if (byte_offset >= SS_TAB_BYTES)
+        for (const dev_blk &b : *c->blocks)
+            if (blk_user(b) == c->d_tab) dst = c->d_tab + b.bytes + (byte_offset - SS_TAB_BYTES);
+    HIPCHK(hipSetDevice(c->device));
+    if (c->launched) HIPCHK(hipStreamWaitEvent(c->hstream, c->done, 0));
+    HIPCHK(hipMemsetAsync(dst, value & 0xff, 1, c->hstream));
+    HIPCHK(hipStreamSynchronize(c->hstream));
     return SS_OK;
 }
 
@@ -419,11 +626,11 @@ static int ensure_stage(ss_ctx_t *c, size_t bytes)
     HIPCHK(hipStreamSynchronize(c->hstream));
     pinned_free(c->h_stage);
     c->h_stage_sz = 0;
-    dev_free(c->d_stage, c->hstream);
+    dev_release(c, c->d_stage, true);           /* its stream is idle: reusable now */
     c->d_stage_sz = 0;
     if (!(c->h_stage = pinned_alloc(sz))) return SS_E_NOMEM;
     c->h_stage_sz = sz;
-    if (dev_alloc(&c->d_stage, sz, c->hstream)) return SS_E_NOMEM;
+    if (int rc = dev_alloc(c, &c->d_stage, sz, c->hstream)) return rc;
     c->d_stage_sz = sz;
     return SS_OK;
 }
@@ -493,9 +700,9 @@ extern "C" int ss_score_batch_host(ss_ctx_t *c, const ss_batch_t *b, const ss_ou
     const size_t o_calls = off; off = align_up(off + sizeof(ss_call_t) * (size_t)cap);
     const size_t o_glf = off;   off = align_up(off + (o->glf ? sizeof(ss_glf_t) * 2 * n : 0));
     const size_t total = off;
+    HIPCHK(hipSetDevice(c->device));
     int rc = ensure_stage(c, total);
     if (rc) return rc;
-    HIPCHK(hipSetDevice(c->device));
     char *h = (char *)c->h_stage, *d = (char *)c->d_stage;
     hipStream_t s = c->hstream;
     /* inputs already in page-locked memory go to the device directly; the
@@ -572,9 +779,10 @@ extern "C" int ss_synth_batch_device(ss_ctx_t *c, const ss_synth_t *s, uint64_t 
     if (!rt || !rn) {
         /* pass 1: depths -> exclusive scans -> offsets */
         if (c->depth_tmp_n < 2 * (n + 1)) {
-            dev_free(*(void **)&c->d_depth_tmp, st);
+            HIPCHK(hipStreamSynchronize(st));
+            dev_release(c, *(void **)&c->d_depth_tmp, true);
             c->depth_tmp_n = 0;
-            if (dev_alloc((void **)&c->d_depth_tmp, 2 * (n + 1) * 4, st)) return SS_E_NOMEM;
+            if (int e = dev_alloc(c, (void **)&c->d_depth_tmp, 2 * (n + 1) * 4, st)) return e;
             c->depth_tmp_n = 2 * (n + 1);
         }
         uint32_t *dt = c->d_depth_tmp, *dn = c->d_depth_tmp + (n + 1);
@@ -583,9 +791,10 @@ extern "C" int ss_synth_batch_device(ss_ctx_t *c, const ss_synth_t *s, uint64_t 
         size_t need = 0;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, dt, off_t, (int)(n + 1), st));
         if (need > c->scan_tmp_sz) {
-            dev_free(c->d_scan_tmp, st);
+            HIPCHK(hipStreamSynchronize(st));
+            dev_release(c, c->d_scan_tmp, true);
             c->scan_tmp_sz = 0;
-            if (dev_alloc(&c->d_scan_tmp, need, st)) return SS_E_NOMEM;
+            if (int e = dev_alloc(c, &c->d_scan_tmp, need, st)) return e;
             c->scan_tmp_sz = need;
         }
         size_t sz = c->scan_tmp_sz;

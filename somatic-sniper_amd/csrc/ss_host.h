@@ -22,6 +22,7 @@ typedef struct ss_host_model {
     int32_t  prior[16 * 10];
     int32_t  jprior[16 * 10 * 10];
     uint64_t h_fk, h_coef, h_lhet;
+    uint64_t fp_coef, fp_lhet; /* ss_tab_fp_words of coef / lhet at their device word offsets */
     int      pinned;        /* default tables equal a pinned reference run */
     int      source;        /* SS_TABLES_BUILT / _PROCESS / _DISK                */
     void    *shared;        /* the process-wide table entry coef / lhet belong to */
@@ -33,6 +34,13 @@ extern const int ss_genotype_nt16[10];
 int      ss_host_model_build(const ss_params_t *p, ss_host_model_t *m);
 void     ss_host_model_free(ss_host_model_t *m);
 uint64_t ss_fnv1a64(const void *p, size_t n);
+
+/* Fingerprint of a device table image (ss_kernels.h SS_TAB_* layout, 8-byte
+ * words): sum over words of mix(w + word_index * golden); additive, so
+ * regions can be summed separately.  Word offsets of the big tables: */
+#define SS_FP_COEF_WORD ((uint64_t)0)
+#define SS_FP_LHET_WORD ((uint64_t)64 << 16)
+uint64_t ss_tab_fp_words(const void *p, size_t nwords, uint64_t first_word);
 
 #ifdef __cplusplus
 }

@@ -98,6 +98,8 @@ struct ss_score_args {
 /* Launchers (return hipError_t as int). */
 int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, hipStream_t s,
                     const hipEvent_t *ev /* 4 events (before main, after main, after wide, after deep) or null */);
+/* out3 (zeroed by the caller): fingerprint sums of coef, lhet and the rest (ss_host.h) */
+int ss_launch_tab_fingerprint(const uint8_t *tab, unsigned long long *out3, hipStream_t s);
 int ss_launch_synth_depth(const ss_synth_k_t &k, uint64_t first, uint64_t n, uint8_t *ref,
                           uint32_t *dt, uint32_t *dn, hipStream_t s);
 int ss_launch_synth_reads(const ss_synth_k_t &k, uint64_t first, uint64_t n,

@@ -154,10 +154,13 @@ __device__ __forceinline__ float geno_p(int j, int k, const float es[4], const f
     const double lh = hom ? 0.0 : -4.343 * ss_tab_lhet(m)[c[j] << 8 | c[k]];
     float v;
     if (c2) {
-        /* the reference's layout, kept on the device: rescaled counts can sum
-         * to 256, and tot = 256 then reads row q + 1, n = 0 exactly as the
-         * reference does (a transposed, q-minor copy measured no faster and
-         * broke that aliasing) */
+        /* the reference's layout and index, kept on the device: rescaled
+         * counts can sum to 256, and tot << 8 is then bit 16, which the OR
+         * merges into bar_e << 16 (sniper_maqcns.c:195,206): an odd bar_e
+         * keeps its row, an even one reads row bar_e + 1, both at n = 0 (a
+         * row sniper_cal_coef leaves zero); bar_e = 63 stays in the table.
+         * (A transposed, q-minor copy measured no faster and broke that
+         * aliasing.) */
         const double cf = ss_tab_coef(m)[(uint32_t)clamp_bar_e(e, f) << 16 | tot << 8 | c2];
         v = hom ? (float)((double)e + cf) : (float)((lh + (double)e) + cf);
     } else {
@@ -1967,8 +1970,53 @@ __global__ void ss_synth_reads_kernel(ss_synth_k_t k, uint64_t first, uint64_t n
 }
 
 /* --------------------------------------------------------------------------
+ * Table fingerprint: the context's device table image as three position-keyed
+ * word sums (coef, lhet, everything after lhet), the same function as the
+ * host's ss_tab_fp_words (ss_tables.c).  ss_ctx_create and ss_ctx_check compare
+ * them with the host's sums, so a device table that no longer holds what was
+ * uploaded is reported (SS_E_TABLES) instead of scoring silently wrong.
+ * ------------------------------------------------------------------------ */
+__device__ __forceinline__ unsigned long long fp_mix(unsigned long long x)
+{
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void ss_tab_fingerprint(const unsigned long long *w, unsigned long long *out)
+{
+    constexpr size_t NW = SS_TAB_BYTES / 8, W_LHET = SS_TAB_LHET / 8, W_REST = SS_TAB_FK / 8;
+    unsigned long long s0 = 0, s1 = 0, s2 = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < NW; i += (size_t)gridDim.x * blockDim.x) {
+        const unsigned long long v = fp_mix(w[i] + (unsigned long long)i * 0x9e3779b97f4a7c15ull);
+        if (i < W_LHET) s0 += v;
+        else if (i < W_REST) s1 += v;
+        else s2 += v;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_xor(s0, o);
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+    }
+    if ((threadIdx.x & 63u) == 0u) {
+        atomicAdd(&out[0], s0);
+        atomicAdd(&out[1], s1);
+        atomicAdd(&out[2], s2);
+    }
+}
+static_assert(SS_TAB_BYTES % 8 == 0 && SS_TAB_LHET % 8 == 0 && SS_TAB_FK % 8 == 0, "table words");
+
+/* --------------------------------------------------------------------------
  * launchers
  * ------------------------------------------------------------------------ */
+int ss_launch_tab_fingerprint(const uint8_t *tab, unsigned long long *out3, hipStream_t s)
+{
+    hipLaunchKernelGGL(ss_tab_fingerprint, dim3(1024), dim3(256), 0, s, (const unsigned long long *)tab, out3);
+    return (int)hipGetLastError();
+}
+
 int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, hipStream_t s,
                     const hipEvent_t *ev)
 {

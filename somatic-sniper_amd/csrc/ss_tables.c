@@ -104,6 +104,31 @@ uint64_t ss_fnv1a64(const void *p, size_t n)
     return h;
 }
 
+/* Position-keyed word sum (ss_kernels.hip ss_tab_fingerprint computes the same
+ * on the device, in any order): word i of the device table image contributes
+ * mix(w + i * golden).  Used to verify that a context's device tables still
+ * hold what was uploaded (ss_ctx_create, ss_ctx_check). */
+static uint64_t fp_mix(uint64_t x)
+{
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+uint64_t ss_tab_fp_words(const void *p, size_t nwords, uint64_t first_word)
+{
+    const unsigned char *b = (const unsigned char *)p;
+    uint64_t s = 0, w;
+    size_t i;
+    for (i = 0; i < nwords; ++i) {
+        memcpy(&w, b + 8 * i, 8);
+        s += fp_mix(w + (first_word + i) * 0x9e3779b97f4a7c15ull);
+    }
+    return s;
+}
+
 /* ---------------------------------------------------------------- coef ---- */
 typedef struct {
     ss_host_model_t *m;
@@ -294,6 +319,7 @@ typedef struct tab_entry {
     float q_r;
     int q_r_int;
     uint64_t h_fk, h_coef, h_lhet;
+    uint64_t fp_coef, fp_lhet;           /* ss_tab_fp_words at their device offsets */
     struct tab_entry *next;
 } tab_entry_t;
 
@@ -486,6 +512,8 @@ static int tab_get(const ss_params_t *p, tab_entry_t **out, int *source)
         blob_store(&k, t);
         *source = SS_TABLES_BUILT;
     }
+    t->fp_coef = ss_tab_fp_words(t->coef, SS_COEF_N, SS_FP_COEF_WORD);
+    t->fp_lhet = ss_tab_fp_words(t->lhet, SS_LHET_N, SS_FP_LHET_WORD);
     t->next = g_tabs;
     g_tabs = t;
     *out = t;
@@ -512,6 +540,8 @@ int ss_host_model_build(const ss_params_t *p, ss_host_model_t *m)
     m->h_fk = t->h_fk;
     m->h_coef = t->h_coef;
     m->h_lhet = t->h_lhet;
+    m->fp_coef = t->fp_coef;
+    m->fp_lhet = t->fp_lhet;
     m->shared = t;
     m->source = source;
     g_last_source = source;

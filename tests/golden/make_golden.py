@@ -14,7 +14,7 @@ The reference is driven exactly as sniper_pileup.c:256-258 calls glf_somatic
 somatic-sniper_amd/csrc/ss_synth.c plus hand-built quirk sites (SURVEY.md
 Appendix A).
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [case ...]
 """
 import os
 import sys
@@ -56,7 +56,10 @@ def main():
     pkg = load_package()
     if not os.path.exists(ob.REF_HARNESS):
         sys.exit("build the reference first: make -f oracle/ref.mk")
+    only = set(sys.argv[1:])                  # case names to regenerate (default: all)
     for name, b, sets in cases(pkg):
+        if only and name not in only:
+            continue
         out = {"ref": b.ref, "off_tumor": b.off_tumor, "off_normal": b.off_normal,
                "reads_tumor": b.reads_tumor, "reads_normal": b.reads_normal}
         with tempfile.TemporaryDirectory() as d:

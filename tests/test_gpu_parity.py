@@ -325,6 +325,26 @@ def quirk_sites(pkg):
     for nt_, nn_ in ((10, 10), (300, 300), (1500, 1000)):
         s.append(("A", [R(60, 30, A)] * nt_,
                   [R(255, 255, T, 1)] * (nn_ // 2) + [R(255, 255, T, i & 1) for i in range(nn_ - nn_ // 2)]))
+    # Rescaled counts summing to 256 (sniper_maqcns.c:178-182: four classes of
+    # odd counts over 508 reads round 63.5 -> 64 each; 2540 = 4 x 635 likewise):
+    # the coef index bar_e<<16 | c<<8 | tmp2 (:195, :206) then ORs bit 16 into
+    # bar_e<<16 -- an odd bar_e keeps its row, an even one moves to bar_e + 1,
+    # n = 0 in both, and bar_e = 63 stays in the table.  Quality q gives
+    # bar_e = q: even (30), odd (31, 45), 63, and 70 clamped to 63 (minq >= 64:
+    # the deep kernel); 508 reads per sample go to the group kernel, 2540 to
+    # the deep kernel; the last site has unequal odd counts (201/101/103/103)
+    # and is a candidate (SSC 4 at default options).
+    def c256(q, per, bases=(A, C_, G, T), mq=None):
+        out = []
+        for b_, n_ in zip(bases, per):
+            out += [R(q if mq is None else mq, q, b_, i & 1) for i in range(n_)]
+        return out
+    s.append(("A", c256(30, (127,) * 4, mq=60), c256(31, (127,) * 4, mq=60)))
+    s.append(("C", c256(63, (127,) * 4), c256(31, (127,) * 4, mq=60)))
+    s.append(("G", c256(30, (635,) * 4, mq=60), c256(63, (635,) * 4)))
+    s.append(("T", c256(70, (127,) * 4), c256(45, (127,) * 4, mq=60)))
+    s.append(("A", c256(40, (201, 101, 103, 103), bases=(T, A, C_, G), mq=60),
+              c256(40, (201, 101, 103, 103), bases=(A, C_, G, T), mq=60)))
     return s
 
 
@@ -335,6 +355,25 @@ def test_quirk_parity(pkg, oracle, opts):
     assert score[9] == -1 and score[10] == -1     # empty packed sample
     assert score[11] == -1                        # ref N
     assert score[12] == 255                       # ref n: scored, not a candidate
+
+
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"]])
+def test_quirks_match_real_reference_on_this_host(pkg, tmp_path, opts):
+    """The hand-built quirk sites (Appendix A, the sum-of-counts-256 coef index
+    included) through the compiled reference on THIS machine vs the GPU."""
+    import os
+    from oracle import binding as ob
+    if not os.path.exists(ob.REF_HARNESS):
+        pytest.skip("reference harness not built")
+    b = pkg.Batch.from_sites(quirk_sites(pkg))
+    path = str(tmp_path / "q.ssb")
+    ob.write_ssb(path, b.ref, b.off_tumor, b.off_normal, b.reads_tumor, b.reads_normal)
+    rec, txt = ob.run_ref_dump(path, opts, str(tmp_path))
+    with pkg.Context(params_from_opts(pkg, opts)) as c:
+        score, calls, glf = c.score_batch(b, want_glf=True)
+    assert (score == rec["ret"]).all(), np.nonzero(score != rec["ret"])
+    assert (glf.view(np.uint8) == rec["glf"].view(np.uint8)).all()
+    assert len(calls) == txt.count("\n")
 
 
 def test_device_synth_matches_host(pkg, ctx):

@@ -12,10 +12,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import bamgen  # noqa: E402
 
-NATIVE = os.path.join(ROOT, "somatic-sniper_amd", "bam-somaticsniper")
+NATIVE = os.path.join(ROOT, os.environ.get("REPRO_NATIVE", "somatic-sniper_amd/bam-somaticsniper"))
 REF_CLI = os.path.join(ROOT, "oracle", "_ref", "bam-somaticsniper")
 INDEX = os.path.join(ROOT, "somatic-sniper_amd", "ss-index")
-OUT = os.path.join(ROOT, "gpurun_out", "repro")
+OUT = os.path.join(ROOT, "gpurun_out", os.environ.get("REPRO_OUT", "repro"))
 
 
 def main():
@@ -45,8 +45,8 @@ def main():
             bad += 1
             open(os.path.join(OUT, f"bad{r}.out"), "w").write(nat)
             open(os.path.join(OUT, f"bad{r}.err"), "w").write(p.stderr)
-        elif r == 0:
-            open(os.path.join(OUT, "good0.err"), "w").write(p.stderr)
+        elif r == 0 or os.environ.get("REPRO_KEEP_ALL") == "1":
+            open(os.path.join(OUT, f"good{r}.err"), "w").write(p.stderr)
         print(f"run {r}: {'ok' if ok else 'MISMATCH'} rc={p.returncode} lines nat={nat.count(chr(10))} "
               f"ref={ref.count(chr(10))}", flush=True)
     print("mismatches", bad, "of", reps)
