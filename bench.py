@@ -25,13 +25,18 @@ directly as ``bench.py --gpus N``: the parent then starts N fresh rank
 processes itself before anything touches the GPU, stays GPU-free, and relays
 rank 0's line.
 
-Extra fields: "roofline" (the kernel with the most time, HIP events over the
-timed region's launches, algorithmic bytes 4 B/read + 16 B/site per launch),
+Extra fields, all measured by rank 0 after the timed region at EVERY N (so
+each line of a 1/2/4/8-GPU scaling run carries them): "roofline" (the kernel
+with the most time, HIP events over the timed region's launches, algorithmic
+bytes 4 B/read + 16 B/site per launch; "traffic" and "valu" from rocprofv3
+--pmc passes over a child scoring rank 0's own first launches of this N),
 "cpu_baseline" (the real reference glf_somatic compiled from source,
-oracle/_ref/ref_harness, 1 core, rank 0 at N=1 only, on a bounded sample of
-the same synthetic workload -- about the same CPU time at any depth --, also
-used as a parity spot check) and "cpu_baseline_all_cores" (the same on every
-core we may use, one process per core).
+oracle/_ref/ref_harness, 1 core, on a bounded sample of the same synthetic
+workload -- about the same CPU time at any depth --, also used as a parity
+spot check), "cpu_baseline_all_cores" (the same on every core we may use, one
+process per core) and "host_fed" (ss_score_batch_host, the PCIe-inclusive
+path a BAM-driven caller uses, on pageable and page-locked host arrays of the
+same workload; never `value`).
 """
 from __future__ import annotations
 
@@ -52,27 +57,28 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "pileup sites/sec at 60\u00d7T/30\u00d7N; 1\u21928 GPU scaling; achieved HBM GB/s vs roofline"
 
 
-def cpu_baseline(lt, ln, sample, seed, gpu_scores_prefix):
+def cpu_baseline(lt, ln, sample, seed, gpu_scores_prefix, shard=0):
     """Time the reference's glf_somatic (compiled from /root/reference) on `sample`
-    sites of shard 0; falls back to the CPU port when the binary is absent."""
+    sites of synth shard `shard` (rank 0's first contig); falls back to the CPU
+    port when the binary is absent."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     scores_path = os.path.join("/tmp", f"ss_cpu_scores_{os.getpid()}.bin")
     if os.path.exists(harness):
         out = subprocess.run([harness, "synth", str(lt), str(ln), str(sample), "--seed", str(seed),
-                              "--shard", "0", "--scores", scores_path],
+                              "--shard", str(shard), "--scores", scores_path],
                              check=True, capture_output=True, text=True).stdout
         r = json.loads(out.strip().splitlines()[-1])
         kind, value = "reference", r["sites_per_s"]
         cpu_scores = np.fromfile(scores_path, np.int32)
         os.unlink(scores_path)
-        desc = (f"{sample} synthetic sites ({lt}xT/{ln}xN, synth shard 0 from site 0: the first positions of "
-                f"contig 0 of the c4 workload / of rank 0's batch 0 of the shard workload), reference glf_somatic "
-                f"only (pileups prebuilt, BAM decode excluded), 1 thread")
+        desc = (f"{sample} synthetic sites ({lt}xT/{ln}xN, synth shard {shard} from site 0: the first positions of "
+                f"rank 0's first contig of the c4 workload / of rank 0's batch 0 of the shard workload), reference "
+                f"glf_somatic only (pileups prebuilt, BAM decode excluded), 1 thread")
     else:
         from __graft_entry__ import load_package
         from oracle import binding as ob
         pkg = load_package()
-        h = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=seed), 0, sample)
+        h = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=seed, shard=shard), 0, sample)
         o = ob.Oracle()
         t0 = time.perf_counter()
         cpu_scores, _, _ = o.score_batch(h.ref, h.off_tumor, h.off_normal, h.reads_tumor,
@@ -110,6 +116,49 @@ def cpu_baseline_all_cores(lt, ln, seed, per_proc=500_000):
             "host_cpus": os.cpu_count(),
             "sample": f"{cores} concurrent processes x {per_proc} synthetic sites ({lt}xT/{ln}xN, own shard each), "
                       f"reference glf_somatic only, total sites / longest process time"}
+
+
+def host_fed(ctx, pkg, args, dev, reps=3):
+    """The PCIe-inclusive rate of ss_score_batch_host (host arrays -> H2D ->
+    kernels -> D2H -> calls sorted), the entry point a BAM-driven caller of
+    bam_sspileup_file -> glf_somatic uses (sniper_pileup.c:226-266).  The
+    batch is the first --host-fed-sites sites of synth shard 0 at the bench's
+    depths, generated on the device and copied to host memory once; then
+    timed from pageable numpy arrays (staged by the library) and from
+    ss_host_alloc (page-locked) arrays.  Best of `reps` calls each; the
+    scores are checked against the device path on the same sites."""
+    import torch
+    n = args.host_fed_sites
+    d = ctx.synth_device(pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=0), 0, n, device=dev)
+    dev_score = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
+                     score=dev_score)
+    torch.cuda.synchronize(dev)
+    nt, nn = d["n_reads"]
+    hb = pkg.Batch(d["ref"].cpu().numpy(), d["off_tumor"].cpu().numpy().view(np.uint32),
+                   d["off_normal"].cpu().numpy().view(np.uint32),
+                   d["reads_tumor"][:nt].cpu().numpy().view(np.uint32),
+                   d["reads_normal"][:nn].cpu().numpy().view(np.uint32))
+    want = dev_score.cpu().numpy()
+    del d, dev_score
+    torch.cuda.empty_cache()
+    in_bytes = hb.ref.nbytes + hb.off_tumor.nbytes + hb.off_normal.nbytes + hb.reads_tumor.nbytes + \
+        hb.reads_normal.nbytes
+    out = {"unit": "sites/s", "sites_per_call": n, "input_bytes_per_call": in_bytes,
+           "output_bytes_per_call": 4 * n, "parity_vs_device_path": True}
+    for kind, b in (("pageable", hb), ("pinned", hb.pinned())):
+        got = ctx.score_batch(b)[0]                    # warm-up: staging areas, first launch
+        out["parity_vs_device_path"] &= bool((got == want).all())
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ctx.score_batch(b)
+            ts.append(time.perf_counter() - t0)
+        out[kind] = {"value": round(n / min(ts), 1), "mean": round(n / float(np.mean(ts)), 1),
+                     "h2d_GBps": round(in_bytes / min(ts) / 1e9, 2), "ms_per_call": round(min(ts) * 1e3, 3)}
+    out["note"] = ("PCIe-inclusive (H2D of the packed batch, kernels, D2H of the scores and calls), one call at a "
+                   "time on one context; `value` is the HBM-resident rate")
+    return out
 
 
 # tuning / diagnostic switches of earlier builds: refused so that no timed run
@@ -190,9 +239,10 @@ PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
 
 
 def pmc_child(args):
-    """--pmc-child: the bench's own launches (rank 0 of a 1-GPU run: the first
-    --pmc-batches c4 launches, or the shard workload's batch 0), scored
-    --pmc-launches passes, nothing else (run under rocprofv3 by live_counters)."""
+    """--pmc-child: the bench's own launches (rank 0's of an --pmc-world-GPU
+    run: its first --pmc-batches c4 launches, or the shard workload's batch 0),
+    scored --pmc-launches passes, nothing else (run under rocprofv3 by
+    live_counters)."""
     import torch
     from __graft_entry__ import load_package
     pkg = load_package()
@@ -200,7 +250,7 @@ def pmc_child(args):
     ctx = pkg.Context(pkg.Params.default(), device=0)
     if args.workload == "shard":
         args.batches = 1
-    batches = make_batches(ctx, pkg, args, 0, 1, dev, limit=args.pmc_batches)
+    batches = make_batches(ctx, pkg, args, 0, args.pmc_world, dev, limit=args.pmc_batches)
     scores = [torch.empty(max(1, d["n_sites"]), dtype=torch.int32, device=dev) for d in batches]
     for _ in range(args.pmc_launches):
         for d, sc in zip(batches, scores):
@@ -234,7 +284,8 @@ def live_counters(args, kernel="ss_score_main"):
                    *(["--c4-scale", str(args.c4_scale)] if args.c4_scale is not None else []),
                    "--chunk", str(args.chunk), "--sites", str(args.sites),
                    "--lt", str(args.lt), "--ln", str(args.ln), "--seed", str(args.seed),
-                   "--pmc-launches", str(args.pmc_launches), "--pmc-batches", str(args.pmc_batches)]
+                   "--pmc-launches", str(args.pmc_launches), "--pmc-batches", str(args.pmc_batches),
+                   "--pmc-world", str(args.pmc_world)]
             # own process group: a pass that overruns is killed with its python child
             proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                     text=True, start_new_session=True)
@@ -259,11 +310,18 @@ def live_counters(args, kernel="ss_score_main"):
                     if re.search(re.escape(kernel) + r"[<(]", row["Kernel_Name"]):
                         d = per.setdefault(int(row["Dispatch_Id"]), {})
                         d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+                        # the dispatch's duration in this same profiled pass (ns)
+                        d["_dur_ns"] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
             # one pass = one launch per batch; the first pass (cold tables) is dropped
             n_pass = len(per) // max(1, args.pmc_launches)
             ds = sorted(per)[n_pass:] or sorted(per)
             for c in counters:
                 vals[c] = float(np.mean([per[k].get(c, 0.0) for k in ds]))
+            if "GRBM_GUI_ACTIVE" in counters:
+                # busy cycles per XCD / duration, both of the same profiled dispatches
+                vals["_clock_ghz"] = float(np.mean([per[k]["GRBM_GUI_ACTIVE"] / 8.0 / per[k]["_dur_ns"]
+                                                    for k in ds if per[k].get("_dur_ns", 0) > 0]))
+                vals["_dur_ms_profiled"] = float(np.mean([per[k]["_dur_ns"] for k in ds])) / 1e6
             vals["_sites_per_launch"] = sites_per_launch(args)
         except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
             print(f"bench: PMC pass {counters} failed: {e}", file=sys.stderr)
@@ -274,10 +332,10 @@ def live_counters(args, kernel="ss_score_main"):
 
 
 def sites_per_launch(args) -> float:
-    """Mean sites per launch of the PMC child's workload (rank 0 of one GPU)."""
+    """Mean sites per launch of the PMC child's workload (rank 0's of --pmc-world GPUs)."""
     if args.workload == "shard":
         return float(args.sites)
-    launches = c4_launches(args.c4_scale, 1, 0, args.chunk)[:args.pmc_batches]
+    launches = c4_launches(args.c4_scale, args.pmc_world, 0, args.chunk)[:args.pmc_batches]
     return sum(n for pieces in launches for _, _, n in pieces) / len(launches)
 
 
@@ -315,15 +373,20 @@ def site_bytes(lt: float, ln: float) -> float:
     return 4.0 * (lt + ln) + 4 + 4 + 1 + 4
 
 
+# a context's own device memory (ss_capi.hip): the model tables (SS_TAB_BYTES)
+# and the group kernel's fold-record buffers (n_CU x 12 waves x SS_GRP_REC_BYTES)
+CTX_BYTES = 34_092_160 + 256 * 12 * (131072 + 128)
+
+
 def c4_rank_bytes(scale: int, world: int, lt: float, ln: float, chunk: int):
     """Planned resident HBM bytes of each rank's C4 share: its sites, plus the
     working set of its largest launch (the context's deep lists, 8 B per site,
-    and the generator's depth arrays, 8 B per site)."""
+    and the generator's depth arrays, 8 B per site) and the context itself."""
     _, sizes, plan = c4_layout(scale, world)
     out = []
     for p in plan:
         n = sum(sizes[t] for t in p)
-        out.append(n * site_bytes(lt, ln) + 16.0 * min(chunk, n))
+        out.append(n * site_bytes(lt, ln) + 16.0 * min(chunk, n) + CTX_BYTES)
     return out
 
 
@@ -471,6 +534,10 @@ def main():
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-launches", type=int, default=3, help=argparse.SUPPRESS)
     ap.add_argument("--pmc-batches", type=int, default=2, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-world", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--no-host-fed", action="store_true", help="skip the host-fed (PCIe-inclusive) sub-line")
+    ap.add_argument("--host-fed-sites", type=int, default=1 << 22,
+                    help="sites per ss_score_batch_host call of the host-fed sub-line")
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
@@ -600,14 +667,17 @@ def main():
         names, sizes, plan = c4_layout(args.c4_scale, world)
         me["contigs"] = [names[t] for t in plan[rank]]
 
-    # GPU scores the CPU baseline is checked against: the first sites of synth
-    # shard 0 (c4: contig 0, position 0 on; shard: rank 0's batch 0)
+    # GPU scores the CPU baseline is checked against: the first sites of this
+    # rank's first launch (c4: its first contig from position 0, synth shard =
+    # that contig; shard: batch 0, synth shard = rank)
     sample = depth_scaled(2_000_000, args.lt, args.ln) if args.cpu_sample is None else args.cpu_sample
-    pre = None
-    for k, d in enumerate(batches):
-        if d["tid"] == 0 and d["first"] == 0:
-            sample = min(sample, d["n_sites"])
-            pre = score[k][:sample].cpu().numpy()
+    pre, cpu_shard = None, 0
+    if batches and batches[0]["first"] == 0:
+        d0 = batches[0]
+        n0 = d0["pieces"][0][2] if c4 else d0["n_sites"]       # the first contig's sites in that launch
+        sample = min(sample, n0)
+        pre = score[0][:sample].cpu().numpy()
+        cpu_shard = d0["tid"]
     reads_all = float(np.sum(reads))
     sites_all = sum(d["n_sites"] for d in batches)
     n_batches = len(batches)
@@ -713,11 +783,13 @@ def main():
     }
     if strong:
         result["strong_scaling"] = strong
-    if rank == 0 and world == 1 and not args.no_pmc:
+    if rank == 0 and not args.no_pmc:
         # live counters of the dominant kernel on this same workload (separate
-        # rocprofv3 passes after the timed region; MI355X_MICROARCH.md: FETCH_SIZE
-        # reports half the streamed read bytes on gfx950 and is doubled, both KiB;
-        # SQ_* wave counters, GRBM_GUI_ACTIVE = busy cycles summed over 8 XCDs)
+        # rocprofv3 passes after the timed region, over a child scoring rank 0's
+        # own first launches of this N; MI355X_MICROARCH.md: FETCH_SIZE reports
+        # half the streamed read bytes on gfx950 and is doubled, both KiB; SQ_*
+        # wave counters, GRBM_GUI_ACTIVE = busy cycles summed over 8 XCDs)
+        args.pmc_world = world
         pc = live_counters(args, result["roofline"]["kernel"])
         if pc:
             rd, wr = 2.0 * pc["FETCH_SIZE"] * 1024.0, pc["WRITE_SIZE"] * 1024.0
@@ -744,12 +816,18 @@ def main():
                 "wave_cycles_split": {k: round(pc[c] / pc["SQ_WAVE_CYCLES"], 3) for k, c in
                                       (("issue", "SQ_ACTIVE_INST_ANY"), ("issue_stall", "SQ_WAIT_INST_ANY"),
                                        ("waitcnt", "SQ_WAIT_ANY"))} if pc["SQ_WAVE_CYCLES"] else None,
-                "clock_ghz_est": round(cyc / (avg_kernel_ms * 1e-3) / 1e9, 3) if avg_kernel_ms else None,
-                "source": "rocprofv3 --pmc, separate passes over a child scoring the same launches: "
+                "clock_ghz_profiled": round(pc["_clock_ghz"], 3) if pc.get("_clock_ghz") else None,
+                "kernel_ms_profiled": round(pc["_dur_ms_profiled"], 4) if pc.get("_dur_ms_profiled") else None,
+                "clock_source": "GRBM_GUI_ACTIVE / 8 over the same dispatches' durations in the same profiled "
+                                "pass (End - Start timestamps of rocprofv3's counter records)",
+                "source": "rocprofv3 --pmc, separate passes over a child scoring rank 0's own launches of this N: "
                           "per-launch means of the second pass",
             }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args.lt, args.ln, sample, args.seed, pre)
+            rf["pmc_launch_world"] = world
+    if rank == 0 and not args.no_host_fed:
+        result["host_fed"] = host_fed(ctx, pkg, args, dev)
+    if rank == 0 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.lt, args.ln, sample, args.seed, pre, shard=cpu_shard)
         allc = cpu_baseline_all_cores(args.lt, args.ln, args.seed,
                                       per_proc=depth_scaled(500_000, args.lt, args.ln))
         if allc:

@@ -20,7 +20,8 @@ def test_bench_json_contract():
     launches, the strong-scaling line and the 1-core reference baseline with
     its parity spot check."""
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--c4-scale", "4096", "--steps", "2",
-                        "--warmup", "1", "--cpu-sample", "20000", "--strong-scale", "8192", "--strong-steps", "2"],
+                        "--warmup", "1", "--cpu-sample", "20000", "--strong-scale", "8192", "--strong-steps", "2",
+                        "--host-fed-sites", "262144"],
                        capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
@@ -43,8 +44,13 @@ def test_bench_json_contract():
         assert rf["traffic"] and 0.5 < rf["traffic_over_algorithmic"] < 3.0, rf
         v = rf["valu"]
         assert v["insts_per_site"] > 50 and 0 < v["issue_frac_lower_bound"] < 1.0, v
+        # the clock from the profiled pass's own cycles and durations (never above MI355X's 2.4 GHz)
+        assert 0.5 < v["clock_ghz_profiled"] <= 2.45 and v["kernel_ms_profiled"] > 0, v
     cb = r["cpu_baseline"]
     assert cb["cores"] == 1 and cb["value"] > 0 and cb["parity_vs_gpu"] is True
+    hf = r["host_fed"]                      # PCIe-inclusive ss_score_batch_host, never `value`
+    assert hf["parity_vs_device_path"] is True and hf["pinned"]["value"] > 1e6 and hf["pageable"]["value"] > 1e6
+    assert 0 < hf["pinned"]["h2d_GBps"] < 200 and hf["pinned"]["value"] < r["value"]
     st = r["strong_scaling"]
     assert st["scaling"] == "strong" and st["value"] > 1e8 and st["c4_scale"] == 8192
     assert st["genome_sites_per_step"] == sum(-(-length // 8192) for length in GRCH38)
@@ -123,11 +129,14 @@ def test_bench_c4_ranks_self_spawned_gloo(gpus):
     """--gpus N launched directly, C4 workload: N ranks (sharing the box's one
     GPU under gloo), each scoring the contigs sharding.shard_contigs gives it;
     every contig is scored exactly once, and the whole genome's sites over the
-    max rank time is the value."""
+    max rank time is the value.  Every N's line carries the north star's
+    fields: the reference CPU baseline (rank 0, with its parity check), the
+    PMC traffic of rank 0's own launches of this N, and the host-fed rate."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo",
                         "--c4-scale", "8192", "--steps", "2", "--warmup", "1", "--strong-scale", "16384",
-                        "--strong-steps", "2"], env=env, capture_output=True, text=True, timeout=600)
+                        "--strong-steps", "2", "--cpu-sample", "20000", "--host-fed-sites", "65536"],
+                       env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["n_gpus"] == gpus and len(r["ranks"]) == gpus and r["scaling"] == "strong"
@@ -136,7 +145,14 @@ def test_bench_c4_ranks_self_spawned_gloo(gpus):
     assert sorted(contigs) == sorted(n for n, _ in GRCH38_NAMES) and len(set(contigs)) == 24
     genome = r["config"]["genome_sites_per_step"]
     assert sum(x["sites_per_step"] for x in r["ranks"]) == genome
-    assert r["value"] > 0 and "cpu_baseline" not in r and r["strong_scaling"]["value"] > 0
+    assert r["value"] > 0 and r["strong_scaling"]["value"] > 0
+    cb = r["cpu_baseline"]
+    assert cb["cores"] == 1 and cb["value"] > 0 and cb["parity_vs_gpu"] is True and "cpu_baseline_all_cores" in r
+    assert r["host_fed"]["parity_vs_device_path"] is True
+    import shutil
+    if shutil.which("rocprofv3") or os.path.exists("/opt/rocm/bin/rocprofv3"):
+        rf = r["roofline"]
+        assert rf["traffic"] and 0.5 < rf["traffic_over_algorithmic"] < 3.0 and rf["pmc_launch_world"] == gpus, rf
     worst = max(x["ms_per_step"] for x in r["ranks"])
     assert abs(r["ms_per_step"] - worst) < 1e-3 + 1e-6 * worst
     assert abs(r["value"] - genome * 2 / (worst * 2 * 1e-3)) / r["value"] < 1e-3
