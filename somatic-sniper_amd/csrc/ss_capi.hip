@@ -56,6 +56,7 @@ struct ss_ctx {
     uint32_t deep_cap;
     uint32_t *d_deep_seg;     /* listed segments' first entries, then their main-wave ids */
     uint8_t *d_grp_rec;       /* the group kernel's per-wave fold-record buffers */
+    uint32_t grp_wgs;         /* group-kernel workgroups d_grp_rec holds buffers for */
     /* timing: a pool of events, SS_EV_PER_LAUNCH per launch while enabled */
     int timing;
     std::vector<hipEvent_t> *ev;
@@ -385,8 +386,6 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
     TRY(dev_alloc(c, (void **)&c->d_counters, SS_NCOUNTERS * sizeof(uint32_t), hs));
     TRY(dev_alloc(c, (void **)&c->d_deep_seg, 2 * (size_t)c->n_cu * SS_MAIN_GRID_PER_CU * (SS_MAIN_BLOCK / 64) * sizeof(uint32_t), hs));
     TRY(dev_alloc(c, (void **)&c->d_cdf, 2 * SS_SYNTH_MAXCDF * sizeof(uint32_t), hs));
-    /* one group-kernel workgroup per CU (wide_grid below), one buffer per wave */
-    TRY(dev_alloc(c, (void **)&c->d_grp_rec, (size_t)c->n_cu * (SS_WIDE_BLOCK / 64) * SS_GRP_REC_BYTES, hs));
 #undef TRY
     /* the tables, lists and counters are complete before any launch can use
      * them, and the tables read back as uploaded */
@@ -446,6 +445,22 @@ static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
     return SS_OK;
 }
 
+/* The group kernel's fold-record buffers (SS_GRP_REC_BYTES per wave) for a
+ * grid of `wgs` workgroups, allocated on first need and grown like the work
+ * lists (the old buffers are retired, not reused, until ss_ctx_destroy): a
+ * context that only ever scores small batches holds a few MB, not the
+ * 403 MB of a full grid. */
+static int ensure_grp_cap(ss_ctx_t *c, uint32_t wgs, hipStream_t s)
+{
+    if (wgs <= c->grp_wgs) return SS_OK;
+    dev_release(c, *(void **)&c->d_grp_rec, false);
+    c->grp_wgs = 0;
+    if (int rc = dev_alloc(c, (void **)&c->d_grp_rec, (size_t)wgs * (SS_WIDE_BLOCK / 64) * SS_GRP_REC_BYTES, s))
+        return rc;
+    c->grp_wgs = wgs;
+    return SS_OK;
+}
+
 extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_out_t *o, void *stream)
 {
     if (!c || !b || !o || !o->score) return SS_E_INVAL;
@@ -472,6 +487,12 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     if (c->launched && s != c->last_stream) HIPCHK(hipStreamWaitEvent(s, c->done, 0));
     int rc = ensure_deep_cap(c, nseg * seg_cap, s);
     if (rc) return rc;
+    /* group kernel: one 12-wave workgroup per CU, or fewer when the batch
+     * could not give every wave a chunk (GB = 32 listed sites per chunk) */
+    const uint64_t grp_chunks_max = (b->n_sites + 31u) / 32u;
+    const uint64_t wg_need = (grp_chunks_max + SS_WIDE_BLOCK / 64 - 1) / (SS_WIDE_BLOCK / 64);
+    const int wide_grid = (int)std::min<uint64_t>((uint64_t)c->n_cu, wg_need);
+    if ((rc = ensure_grp_cap(c, (uint32_t)wide_grid, s))) return rc;
     /* counters: deep2, listed segments and entries, the group kernel's next
      * chunk (err is sticky until ss_ctx_check) */
     HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 4 * sizeof(uint32_t), s));
@@ -523,7 +544,6 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         evs = c->ev->data() + SS_EV_PER_LAUNCH * c->n_logged;
         ++c->n_logged;
     }
-    const int wide_grid = c->n_cu;                /* one 8-wave workgroup per CU (d_grp_rec is sized for it) */
     int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, s, evs);
     if (e != 0) return SS_E_HIP;
     HIPCHK(hipEventRecord(c->done, s));

@@ -36,11 +36,14 @@ def params_from_opts(pkg, opts):
 
 
 def assert_parity(pkg, oracle, batch, opts=(), ctx=None):
+    """Every output against the oracle, twice: with glf records requested and
+    without (the way the CLI and the bench score)."""
     own = ctx is None
     if own:
         ctx = pkg.Context(params_from_opts(pkg, opts), device=0)
     try:
         score, calls, glf = ctx.score_batch(batch, want_glf=True)
+        score_x, calls_x, _ = ctx.score_batch(batch, want_glf=False)
     finally:
         if own:
             ctx.close()
@@ -54,6 +57,10 @@ def assert_parity(pkg, oracle, batch, opts=(), ctx=None):
     assert bad.size == 0, f"{bad.size} glf mismatches, first site {bad[0]}: gpu {glf[bad[0]]} oracle {o_glf[bad[0]]}"
     assert len(calls) == len(o_calls)
     assert (calls.view(np.uint8) == o_calls.view(np.uint8)).all()
+    bad = np.nonzero(score_x != o_score)[0]
+    assert bad.size == 0, f"no glf: {bad.size} score mismatches, first {bad[:5]}: gpu {score_x[bad[:5]]} " \
+                          f"oracle {o_score[bad[:5]]}"
+    assert len(calls_x) == len(o_calls) and (calls_x.view(np.uint8) == o_calls.view(np.uint8)).all()
     return score, calls
 
 
@@ -355,6 +362,81 @@ def test_quirk_parity(pkg, oracle, opts):
     assert score[9] == -1 and score[10] == -1     # empty packed sample
     assert score[11] == -1                        # ref N
     assert score[12] == 255                       # ref n: scored, not a candidate
+
+
+def all_reference_sites(pkg):
+    """Sites whose every read is on the reference base (round 5 measured an
+    early exit for them): the count of reads of minq >= 24
+    from 0 to all, at depths 1 .. 128 (the lane path's limit) and 129 (the
+    group kernel); reads that count as the reference only through nt16
+    semantics (N / IUPAC as A, '='); a single non-reference read that does not
+    contribute (q = 0); soft-masked, 'n' and IUPAC references; somatic-looking
+    sites among them; and single-strand low-quality (q 4) sites where another
+    homozygote ties the reference's and sniper_glf2cns calls another base."""
+    R = lambda mq, bq, nt, st=0: _r(pkg, mq, bq, nt, st)
+    A, C_, G, T, N, EQ, M = 1, 2, 4, 8, 15, 0, 3
+    code = {"A": A, "C": C_, "G": G, "T": T}
+    rng = np.random.default_rng(7)
+    s = []
+    for i, n in enumerate([1, 2, 3, 7, 16, 30, 31, 60, 61, 64, 89, 100, 127, 128, 129]):
+        for c24 in sorted({0, 1, max(0, n // 8 - 1), n // 8, n // 4, n}):
+            c24 = min(c24, n)
+            ref = "ACGT"[(i + c24) % 4]
+            b = code[ref]
+            t = [R(60, 24 + int(rng.integers(0, 18)), b, j & 1) for j in range(c24)] + \
+                [R(int(rng.integers(0, 61)), 2 + int(rng.integers(0, 22)), b, j & 1) for j in range(n - c24)]
+            nn = max(1, n // 2)
+            nm = [R(60, 10 + int(rng.integers(0, 30)), b, j & 1) for j in range(nn)]
+            s.append((ref, t, nm))
+    for ref in "ACGT":
+        b = code[ref]
+        s.append((ref, [R(60, 30, N)] * 5 + [R(60, 30, b)] * 40, [R(60, 30, b)] * 30))       # N counts as A
+        s.append((ref, [R(60, 30, M)] * 3 + [R(60, 30, b)] * 40, [R(60, 30, b)] * 30))       # IUPAC counts as A
+        s.append((ref, [R(60, 30, EQ)] * 10 + [R(60, 30, b)] * 40, [R(60, 30, EQ)] * 30))    # '=' is the reference
+        s.append((ref, [R(0, 0, T if b != T else A)] + [R(60, 30, b)] * 40, [R(60, 30, b)] * 30))  # q = 0 non-ref
+        s.append((ref.lower(), [R(60, 30, b)] * 40, [R(60, 30, b)] * 30))                   # soft-masked reference
+        s.append((ref, [R(60, 35, T if b != T else A, j & 1) for j in range(20)], [R(60, 35, b)] * 20))
+    for ch in "nRYMK":
+        s.append((ch, [R(60, 30, A)] * 40, [R(60, 30, A)] * 30))
+    # every read on the reference, one strand, of low quality (q 4): the other
+    # homozygotes' p (esum + coef[bar_e][n][n], coef < 0) rounds to lk 0 and
+    # ties the reference's, and sniper_glf2cns calls another base (18 of these
+    # sites score 0 or 9 in the reference)
+    for ref in "CGT":
+        b = code[ref]
+        for n in (20, 60, 100, 128):
+            s.append((ref, [R(60, 2 + (j % 2), b, 0) for j in range(n)], [R(60, 30, b)] * 30))
+            s.append((ref, [R(60, 30, b)] * 30, [R(60, 2 + (j % 2), b, 1) for j in range(n)]))
+    return s
+
+
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"]])
+def test_all_reference_sites_parity(pkg, oracle, opts):
+    """all_reference_sites against the oracle, with and without glf records,
+    plus a 60x/30x batch with few errors (most sites all-reference)."""
+    batch = pkg.Batch.from_sites(all_reference_sites(pkg))
+    assert_parity(pkg, oracle, batch, opts)
+    clean = pkg.synth_batch_host(pkg.Synth.default(60, 30, seed=77, p_error=0.002, p_nbase=0.0005,
+                                                   p_somatic=0.01, p_germline=0.01), 0, 20000)
+    assert_parity(pkg, oracle, clean, opts)
+
+
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"]])
+def test_all_reference_sites_match_real_reference(pkg, tmp_path, opts):
+    """all_reference_sites through the compiled reference on THIS machine vs
+    the GPU (no glf records requested)."""
+    import os
+    from oracle import binding as ob
+    if not os.path.exists(ob.REF_HARNESS):
+        pytest.skip("reference harness not built")
+    b = pkg.Batch.from_sites(all_reference_sites(pkg))
+    path = str(tmp_path / "e.ssb")
+    ob.write_ssb(path, b.ref, b.off_tumor, b.off_normal, b.reads_tumor, b.reads_normal)
+    rec, txt = ob.run_ref_dump(path, opts, str(tmp_path))
+    with pkg.Context(params_from_opts(pkg, opts)) as c:
+        score, calls, _ = c.score_batch(b, want_glf=False)
+    assert (score == rec["ret"]).all(), np.nonzero(score != rec["ret"])
+    assert len(calls) == txt.count("\n")
 
 
 @pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"]])
