@@ -123,12 +123,14 @@ def host_fed(ctx, pkg, args, dev, reps=3):
     kernels -> D2H -> calls sorted), the entry point a BAM-driven caller of
     bam_sspileup_file -> glf_somatic uses (sniper_pileup.c:226-266).  The
     batch is the first --host-fed-sites sites of synth shard 0 at the bench's
-    depths, generated on the device and copied to host memory once; then
-    timed from pageable numpy arrays (staged by the library) and from
-    ss_host_alloc (page-locked) arrays.  Best of `reps` calls each; the
+    depths (fewer where that many would pass 2^31 reads), generated on the
+    device and copied to host memory once; then timed from pageable numpy
+    arrays (staged by the library) and from ss_host_alloc (page-locked)
+    arrays.  Best of `reps` calls each; the
     scores are checked against the device path on the same sites."""
     import torch
-    n = args.host_fed_sites
+    # at most 2^31 expected reads per sample: u32 read offsets with Poisson headroom
+    n = min(args.host_fed_sites, (1 << 31) // int(max(args.lt, args.ln, 1)))
     d = ctx.synth_device(pkg.Synth.default(args.lt, args.ln, seed=args.seed, shard=0), 0, n, device=dev)
     dev_score = torch.empty(n, dtype=torch.int32, device=dev)
     ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"],
