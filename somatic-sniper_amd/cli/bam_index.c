@@ -59,15 +59,17 @@ bad:
     return NULL;
 }
 
-/* an index older than its BAM is stale (htslib's test, hts.c idx_test_and_fetch):
- * it may describe a file since rewritten, so it is not used */
+/* an index whose mtime is an earlier second than its BAM's is stale: it may
+ * describe a file since rewritten.  htslib makes the same whole-second test
+ * (hts.c idx_test_and_fetch) but only warns and uses the index; here it is not
+ * used and the CLI takes the streaming walk instead (same output, no
+ * contig-parallel pileup).  An index written in the same second as its BAM is
+ * used, as in htslib; bai_check_start still verifies it against the file. */
 static bai_t *bai_load_fresh(const char *idx_path, const struct stat *bam_st)
 {
     struct stat st;
     if (stat(idx_path, &st) != 0) return NULL;
-    if (st.st_mtim.tv_sec < bam_st->st_mtim.tv_sec ||
-        (st.st_mtim.tv_sec == bam_st->st_mtim.tv_sec && st.st_mtim.tv_nsec < bam_st->st_mtim.tv_nsec))
-        return NULL;
+    if (st.st_mtime < bam_st->st_mtime) return NULL;
     return bai_load(idx_path);
 }
 
@@ -88,14 +90,18 @@ bai_t *bai_load_for(const char *bam_path)
     return x;
 }
 
-int bai_check_start(const char *bam_path, uint64_t v, int32_t t0, int32_t n_ref)
+int bai_check_start(const char *bam_path, const bai_t *x, int32_t t0)
 {
-    bgzf_reader_t *fp = bgzf_open_at(bam_path, 0, v);
+    int32_t t = t0 < 0 ? 0 : t0;
+    while (t < x->n_ref && x->ref[t].first == UINT64_MAX) ++t;
+    if (t >= x->n_ref) return 0;                       /* nothing indexed from t0 on */
+    bgzf_reader_t *fp = bgzf_open_at(bam_path, 0, x->ref[t].first);
     if (!fp) return -1;
     bam_record_t rec;
     memset(&rec, 0, sizeof rec);
     const int rc = bam_record_read(fp, &rec);
-    const int ok = rc > 0 && rec.tid >= t0 && rec.tid < n_ref && rec.pos >= -1;
+    /* the record there must be on the contig the index says it starts */
+    const int ok = rc > 0 && rec.tid == t && rec.pos >= -1;
     bam_record_free(&rec);
     bgzf_close(fp);
     return ok ? 0 : -1;
@@ -116,17 +122,21 @@ uint64_t bai_first_at_or_after(const bai_t *x, int32_t t0)
     return UINT64_MAX;
 }
 
-/* records from voffset `start` up to the first one on contig t0 or later:
- * the last that the pileup loads.  1 found, 0 none, -1 read error. */
-static int scan_tail(const char *bam_path, uint64_t start, int32_t t0, uint32_t mask, int thresh,
+/* records from voffset `start` (an index offset of contig t) up to the first
+ * one on contig t0 or later: the last that the pileup loads.  1 found, 0 none,
+ * -1 read error, -2 the first record is not on contig t (the index does not
+ * describe this file). */
+static int scan_tail(const char *bam_path, uint64_t start, int32_t t, int32_t t0, uint32_t mask, int thresh,
                      int32_t *tid, int64_t *pos)
 {
     bgzf_reader_t *fp = bgzf_open_at(bam_path, 0, start);
     if (!fp) return -1;
     bam_record_t rec;
     memset(&rec, 0, sizeof rec);
-    int found = 0, rc;
+    int found = 0, rc, first = 1;
     while ((rc = bam_record_read(fp, &rec)) > 0) {
+        if (first && rec.tid != t) { rc = -2; break; }
+        first = 0;
         if (rec.tid >= t0 || rec.tid < 0) break;
         if ((rec.flag & mask) || rec.mapq < thresh) continue;
         *tid = rec.tid;
@@ -135,7 +145,7 @@ static int scan_tail(const char *bam_path, uint64_t start, int32_t t0, uint32_t 
     }
     bam_record_free(&rec);
     bgzf_close(fp);
-    return rc < 0 ? -1 : found;
+    return rc == -2 ? -2 : rc < 0 ? -1 : found;
 }
 
 int bai_last_loaded_before(const char *bam_path, const bai_t *x, int32_t t0, uint32_t mask, int thresh,
@@ -149,7 +159,7 @@ int bai_last_loaded_before(const char *bam_path, const bai_t *x, int32_t t0, uin
         for (;;) {
             while (i >= 0 && (r->ioff[i] == 0 || r->ioff[i] < r->first)) --i;
             const uint64_t start = i >= 0 ? r->ioff[i] : r->first;
-            const int rc = scan_tail(bam_path, start, t0, mask, thresh, tid, pos);
+            const int rc = scan_tail(bam_path, start, t, t0, mask, thresh, tid, pos);
             if (rc != 0) return rc;
             if (start == r->first) break;                  /* the whole contig: nothing loaded */
             i -= step;

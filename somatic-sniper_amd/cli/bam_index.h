@@ -31,13 +31,16 @@ int bai_build(const char *bam_path, const char *out_path);
  * mapQ >= thresh): its contig and position, found by reading the tail of the
  * last contig before t0 that has records (its last linear-index windows,
  * further back only when none of them passes the filter).  Returns 1 with
- * *tid / *pos, 0 when no such record exists, -1 on a read error. */
+ * *tid / *pos, 0 when no such record exists, -1 on a read error, -2 when a
+ * record at one of the index's offsets is not on the contig the index gives
+ * (an index of another file). */
 int bai_last_loaded_before(const char *bam_path, const bai_t *x, int32_t t0, uint32_t mask, int thresh,
                            int32_t *tid, int64_t *pos);
 /* Virtual offset of the first record of contig t0 or later (UINT64_MAX: none). */
 uint64_t bai_first_at_or_after(const bai_t *x, int32_t t0);
-/* 0 when the record at virtual offset v reads back and lies on a contig in
- * [t0, n_ref): the index agrees with the file there; -1 otherwise. */
-int bai_check_start(const char *bam_path, uint64_t v, int32_t t0, int32_t n_ref);
+/* 0 when the record at the index's first offset of contig t0 or later reads
+ * back and lies on that very contig (or nothing is indexed from t0 on): the
+ * index agrees with the file there; -1 otherwise. */
+int bai_check_start(const char *bam_path, const bai_t *x, int32_t t0);
 
 #endif

@@ -514,8 +514,8 @@ static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq,
         q->v2 = bai_first_at_or_after(x2, q->t0);
         /* an index that does not agree with its file (stale, or another file's)
          * would seek mid-record or to the wrong contig: the streaming walk runs */
-        if ((q->v1 != UINT64_MAX && bai_check_start(bam1, q->v1, q->t0, n_ref)) ||
-            (q->v2 != UINT64_MAX && bai_check_start(bam2, q->v2, q->t0, x2->n_ref))) {
+        if ((q->v1 != UINT64_MAX && bai_check_start(bam1, x1, q->t0)) ||
+            (q->v2 != UINT64_MAX && bai_check_start(bam2, x2, q->t0))) {
             stale = 1;
             break;
         }
@@ -525,9 +525,11 @@ static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq,
         int64_t pos;
         const uint32_t mask = SS_BAM_DEF_MASK;
         int r = bai_last_loaded_before(bam1, x1, q->t0, mask, mapq, &tid, &pos);
+        if (r == -2) { stale = 1; break; }             /* the index is another file's */
         if (r < 0) bad = 1;
         else if (r) { q->s1.has_prev = 1; q->s1.prev_tid = tid; q->s1.prev_pos = pos; }
         r = bai_last_loaded_before(bam2, x2, q->t0, mask, mapq, &tid, &pos);
+        if (r == -2) { stale = 1; break; }
         if (r < 0) bad = 1;
         else if (r) { q->s2.has_prev = 1; q->s2.prev_tid = tid; q->s2.prev_pos = pos; }
         if (timing)

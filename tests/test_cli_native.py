@@ -369,6 +369,12 @@ def test_stale_or_foreign_index_takes_streaming_walk(tmp_path):
     os.utime(dst / (t + ".bai"), ns=(st.st_atime_ns, st.st_mtime_ns - 10 ** 9))
     got, grouped = _grouped_dump(dst, fa, t, n)
     assert got == ref and not grouped
+    # written in the same second as its BAM (whole-second test, as htslib's): used
+    sec = st.st_mtime_ns // 10 ** 9 * 10 ** 9
+    os.utime(dst / t, ns=(st.st_atime_ns, sec + 5 * 10 ** 8))
+    os.utime(dst / (t + ".bai"), ns=(st.st_atime_ns, sec))
+    got, grouped = _grouped_dump(dst, fa, t, n)
+    assert got == ref and grouped
     # foreign: the tumor BAM carries another dataset's index (same contig count)
     dst2 = tmp_path / "foreign"
     assert _indexed_copy(d, fa, t, n, dst2)
