@@ -277,6 +277,8 @@ def live_counters(args, kernel="ss_score_main"):
         return None
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     env["TMPDIR"] = "/tmp"
+    if env.get("SNIPER_AMD_LIB"):                  # the child runs in /tmp: the library the bench loaded
+        env["SNIPER_AMD_LIB"] = os.path.abspath(env["SNIPER_AMD_LIB"])
     vals = {}
     for counters in PMC_PASSES:
         out = tempfile.mkdtemp(prefix="ss_pmc_", dir="/tmp")

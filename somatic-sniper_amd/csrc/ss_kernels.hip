@@ -922,6 +922,8 @@ struct LaneIn {
     uint32_t na, nb, na4;
     uint32_t nca, nab;               /* A's chunks (na4 / 4); na4 + nb */
     uint32_t la, lb;                 /* byte offsets of A's and B's lookup rows (see LN_LUT_BYTES) */
+    uint32_t clast;                  /* CLAMP loads: chunks past this one load it again */
+    uint32_t cstep;                  /* STRIDE: words from one chunk of the lane to its next */
     bool tail;                       /* wave-uniform: an x4 load could pass the end of the reads */
 };
 
@@ -937,12 +939,14 @@ struct LaneAcc {
  * is the instruction's immediate and the loads in flight stay in fixed
  * registers.  In a tail block (the batch's last sites, or a batch of fewer
  * than 4 reads) the lane loads word by word, only its own reads. */
+template <bool CLAMP, bool STRIDE>
 __device__ __forceinline__ void ln_load(const LaneIn &in, uint32_t c, uint32_t (&x)[4])
 {
     const bool fa = c < in.nca;
-    const uint32_t *src = (fa ? in.pa : in.pb) + 4u * c;
+    const uint32_t cc = CLAMP ? min(c, in.clast) : c;
+    const uint32_t *src = (fa ? in.pa : in.pb) + (STRIDE ? cc * in.cstep : 4u * cc);
     if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */
-        const int lim = (int)(fa ? in.na : in.nab) - (int)(4u * c);
+        const int lim = (int)(fa ? in.na : in.nab) - (int)(STRIDE ? c * in.cstep : 4u * c);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             x[t] = 0u;
@@ -965,12 +969,13 @@ __device__ __forceinline__ uint32_t ln_nz(uint32_t x)
 /* keys of chunk c from its loaded words x; rms / group sizes into acc.
  * Elements past the sample's reads are masked to 0 (a non-contributing read);
  * a non-contributing read's lookup offset is multiplied by 0 (entry 0). */
+template <bool STRIDE>
 __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint2 *lut, uint32_t c, uint32_t cap,
                                          const uint32_t (&x)[4], uint32_t (&v)[LN_R], LaneAcc &acc)
 {
     const uint32_t c4 = 4u * c;
     const bool fa = c < in.nca;
-    const int lim = (int)(fa ? in.na : in.nab) - (int)c4;
+    const int lim = (int)(fa ? in.na : in.nab) - (int)(STRIDE ? c * in.cstep : c4);
     uint32_t valid, vl;                             /* bit t: element c4 + t is a read */
     asm("v_med3_i32 %0, %1, 0, 4" : "=v"(vl) : "v"(lim));
     asm("v_bfm_b32 %0, %1, 0" : "=v"(valid) : "v"(vl));
@@ -1017,6 +1022,7 @@ __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint2 *lut, uin
     acc.cnt_a += fa ? ccnt : 0u;
 }
 
+template <bool CLAMP = false, bool STRIDE = false>
 __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint2 *lut, uint32_t nch, uint32_t cap,
                                            uint32_t (&v)[LN_R])
 {
@@ -1030,17 +1036,17 @@ __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint2 *lut, u
     uint32_t buf[2][LN_P][4];
     if (nch > 0u) {
 #pragma unroll
-        for (int j = 0; j < LN_P; ++j) ln_load(in, (uint32_t)j, buf[0][j]);
+        for (int j = 0; j < LN_P; ++j) ln_load<CLAMP, STRIDE>(in, (uint32_t)j, buf[0][j]);
     }
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
         if ((uint32_t)(g * LN_P) >= nch) continue;
         if (g + 1 < NG && (uint32_t)((g + 1) * LN_P) < nch) {
 #pragma unroll
-            for (int j = 0; j < LN_P; ++j) ln_load(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
+            for (int j = 0; j < LN_P; ++j) ln_load<CLAMP, STRIDE>(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
         }
 #pragma unroll
-        for (int j = 0; j < LN_P; ++j) ln_chunk(in, lut, (uint32_t)(g * LN_P + j), cap, buf[g & 1][j], v, acc);
+        for (int j = 0; j < LN_P; ++j) ln_chunk<STRIDE>(in, lut, (uint32_t)(g * LN_P + j), cap, buf[g & 1][j], v, acc);
     }
     /* a high half never keyed stays 0: the complement of the pad key */
     acc.rms_b -= acc.rms_a;          /* totals -> B's share */
@@ -1157,6 +1163,41 @@ __device__ __forceinline__ void ln_chain(const LaneLds &L, uint32_t lane, uint32
         if (i < n) ln_steps<true>(fkb, ln_window(colw, s0 + n - i), n - i, W, e, f);
 }
 
+/* the three groups other than the lane's largest, walked together: one record
+ * of each per step (their chains are usually 0 - 2 records, so this is one or
+ * two steps where three chain loops cost a 4-record step each).  Record i of
+ * a chain is byte (i + 4) & 3 of row (i + 4) >> 2 of the lane's column; past
+ * its end a chain reads fk's zero entry. */
+__device__ __forceinline__ void ln_chain3(const LaneLds &L, uint32_t lane, const uint32_t (&s0)[3],
+                                          const uint32_t (&n)[3], const double *fk, float (&e)[3], float (&f)[3])
+{
+    const uint8_t *col = reinterpret_cast<const uint8_t *>(&L.rec[0][lane]);
+    const char *fkb = reinterpret_cast<const char *>(fk);
+    uint32_t W[3] = {0u, 0u, 0u};
+    const uint32_t mx = max(max(n[0], n[1]), n[2]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { e[k] = 0.0f; f[k] = 0.0f; }
+    for (uint32_t i = 0; __ballot(i < mx); ++i) {
+        uint32_t r[3];
+        double t[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const bool act = i < n[k];
+            const uint32_t b = (act ? s0[k] + n[k] - 1u - i : 0u) + 4u;
+            r[k] = col[(b >> 2) * 256u + (b & 3u)];
+            const uint32_t sh = (r[k] >> 2) & 16u;
+            const uint32_t w8 = __builtin_amdgcn_ubfe(W[k], sh, 16u);
+            W[k] += 8u << sh;
+            t[k] = *reinterpret_cast<const double *>(fkb + (act ? w8 : 8u * LN_FK_ZERO));
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            e[k] = (float)((double)e[k] + t[k] * (double)(r[k] & 63u));
+            f[k] = (float)((double)f[k] + t[k]);
+        }
+    }
+}
+
 /* fold of one sample: group sizes cnt (8-bit fields), records from s0 */
 __device__ __forceinline__ void ln_fold(const LaneLds &L, uint32_t lane, uint32_t s0, uint32_t cnt,
                                         const double *fk, float es[4], float fs[4], uint32_t c[4])
@@ -1174,6 +1215,24 @@ __device__ __forceinline__ void ln_fold(const LaneLds &L, uint32_t lane, uint32_
     float e, f;
     const uint32_t sbig = big == 0 ? st[0] : (big == 1 ? st[1] : (big == 2 ? st[2] : st[3]));
     ln_chain(L, lane, sbig, cb, fk, e, f);
+    /* the other three together, unless one of them is long (a heterozygous
+     * site: then chain by chain, four records per step) */
+    const uint32_t o0 = big == 0u ? 1u : 0u, o1 = big <= 1u ? 2u : 1u, o2 = big <= 2u ? 3u : 2u;
+    const uint32_t so[3] = {o0 == 0u ? st[0] : st[1], o1 == 1u ? st[1] : st[2], o2 == 2u ? st[2] : st[3]};
+    const uint32_t no[3] = {o0 == 0u ? c[0] : c[1], o1 == 1u ? c[1] : c[2], o2 == 2u ? c[2] : c[3]};
+    if (!__ballot(max(max(no[0], no[1]), no[2]) > 6u)) {
+        float eo[3], fo[3];
+        ln_chain3(L, lane, so, no, fk, eo, fo);
+        es[0] = big == 0u ? e : eo[0];
+        fs[0] = big == 0u ? f : fo[0];
+        es[1] = big == 1u ? e : (big == 0u ? eo[0] : eo[1]);
+        fs[1] = big == 1u ? f : (big == 0u ? fo[0] : fo[1]);
+        es[2] = big == 2u ? e : (big <= 1u ? eo[1] : eo[2]);
+        fs[2] = big == 2u ? f : (big <= 1u ? fo[1] : fo[2]);
+        es[3] = big == 3u ? e : eo[2];
+        fs[3] = big == 3u ? f : fo[2];
+        return;
+    }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         float eb, fb;
@@ -1404,6 +1463,10 @@ namespace {
 
 #define GP_WAVES (SS_WIDE_BLOCK / 64)         /* 12 waves, one workgroup per CU (168 VGPRs: 3 per SIMD) */
 #define GP_UNITS (2 * GB)
+/* lane positions of a chunk's units: at most 64 units of <= 16 lanes, packed
+ * by descending size into 64-lane batches that waste < 16 lanes each, so at
+ * most 21 batches (1024 / 49 + 1) */
+#define GP_LANEPOS (21 * 64)
 
 /* Per wave: the chunk's sites and units are kept here, not in registers, so
  * that the sort and merge (64 registers of keys) leave room for 3 waves per
@@ -1420,16 +1483,29 @@ struct alignas(16) GroupLds {
     uint32_t u_off[GP_WAVES][GP_UNITS];            /* its first lane position */
     uint32_t u_base[GP_WAVES][GP_UNITS];           /* its first record byte */
     uint32_t ucnt[GP_WAVES][GP_UNITS][4];          /* per unit: counts of bases 0, 2 | 1, 3 (16-bit), rms, wild */
-    uint8_t  unit_of[GP_WAVES][GP_UNITS * 16];     /* lane position -> unit */
+    uint8_t  unit_of[GP_WAVES][GP_LANEPOS];        /* lane position -> unit (0xff: a lane no unit uses) */
 };
 
-/* cross-lane compare-exchange: the lower lane keeps (min lo, max hi) */
+/* cross-lane compare-exchange of lane j of a unit with its lane j ^ LJ, read
+ * by ds_bpermute from the unit's first lane pb (units need no alignment; the
+ * exchange runs on the LDS crossbar, not the VALU).  The lower lane keeps
+ * (min lo, max hi).  A unit of U lanes sorts as one of P = pow2 >= U lanes
+ * whose lanes U .. P - 1 hold only pads; this lane is then always the lower
+ * one of the pair and must stay as it is (a virtual lane only ever receives
+ * maxima, i.e. pads): it reads itself, which a plain stage leaves unchanged,
+ * and a mirror stage reads the neutral 0x0000ffff instead (pad key low, its
+ * complement high). */
 template <int LJ, bool MIRROR>
-__device__ __forceinline__ void gp_xstage(uint32_t (&v)[LN_R], uint32_t msk)
+__device__ __forceinline__ void gp_xstage(uint32_t (&v)[LN_R], uint32_t j, uint32_t pb, uint32_t U)
 {
+    const uint32_t pj = j ^ (uint32_t)LJ;
+    const bool pad = pj >= U;
+    const int addr = (int)((pb + (pad ? j : pj)) << 2);
+    const uint32_t msk = (j & (MIRROR ? (uint32_t)((LJ + 1) >> 1) : (uint32_t)LJ)) ? 0xffff0000u : 0x0000ffffu;
 #pragma unroll
     for (int r = 0; r < LN_R; ++r) {
-        const uint32_t o = xor_lane<LJ>(v[r]);
+        uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v[r]);
+        if (MIRROR) o = pad ? 0x0000ffffu : o;
         uint32_t mn, mx;
         if (MIRROR) {                        /* partner element 127 - r: swap and complement */
             const uint32_t c = ~o;
@@ -1456,19 +1532,24 @@ __device__ __forceinline__ void gp_stage64(uint32_t (&v)[LN_R])
 
 /* level 128 M of a unit (M lanes merged), lane index j inside the unit */
 template <int M>
-__device__ __forceinline__ void gp_level(uint32_t (&v)[LN_R], uint32_t j)
+__device__ __forceinline__ void gp_level(uint32_t (&v)[LN_R], uint32_t j, uint32_t pb, uint32_t U)
 {
-    gp_xstage<M - 1, true>(v, (j & (uint32_t)(M / 2)) ? 0xffff0000u : 0x0000ffffu);
-    if constexpr (M >= 16) gp_xstage<4, false>(v, (j & 4u) ? 0xffff0000u : 0x0000ffffu);
-    if constexpr (M >= 8) gp_xstage<2, false>(v, (j & 2u) ? 0xffff0000u : 0x0000ffffu);
-    if constexpr (M >= 4) gp_xstage<1, false>(v, (j & 1u) ? 0xffff0000u : 0x0000ffffu);
+    gp_xstage<M - 1, true>(v, j, pb, U);
+    if constexpr (M >= 16) gp_xstage<4, false>(v, j, pb, U);
+    if constexpr (M >= 8) gp_xstage<2, false>(v, j, pb, U);
+    if constexpr (M >= 4) gp_xstage<1, false>(v, j, pb, U);
     gp_stage64(v);
     ln_clean<LN_R, 32>(v);
 }
 
+/* lanes of a unit of n reads (128 each), and the network size it sorts as */
 __device__ __forceinline__ uint32_t gp_lanes(uint32_t n)
 {
-    return n <= 128u ? 1u : n <= 256u ? 2u : n <= 512u ? 4u : n <= 1024u ? 8u : 16u;
+    return n <= 128u ? 1u : (n + 127u) >> 7;
+}
+__device__ __forceinline__ uint32_t gp_pow2(uint32_t U)
+{
+    return U <= 1u ? 1u : U <= 2u ? 2u : U <= 4u ? 4u : U <= 8u ? 8u : 16u;
 }
 
 }  // namespace
@@ -1541,22 +1622,33 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
         wave_sync();
         uint32_t T = 0;
         {
-            /* units: lane u < 2G is unit u = (entry u / 2, sample u & 1); lane
-             * positions by descending U (aligned, so a unit never straddles a
-             * batch), record bases in unit order rounded up to 16 bytes (x4 stores) */
+            /* units: lane u < 2G is unit u = (entry u / 2, sample u & 1) of
+             * U = ceil(n / 128) lanes, packed by descending U into 64-lane
+             * batches (a unit never straddles one; the rest of a batch that
+             * cannot take the next unit stays empty); record bases in unit
+             * order rounded up to 16 bytes (x4 stores) */
             const bool is_u = lane < 2u * G;
             const uint32_t n_u = is_u ? L.u_n[wv][lane] : 0u;
             const uint32_t U_u = gp_lanes(n_u);
             uint32_t off_u = 0;
-#pragma unroll
-            for (uint32_t c = 16u; c >= 1u; c >>= 1) {
+            for (uint32_t c = 16u; c >= 1u; --c) {
                 const uint64_t mk = __ballot(is_u && U_u == c);
-                if (is_u && U_u == c)
-                    off_u = T + c * __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-                T += c * (uint32_t)__popcll(mk);
+                if (!mk) continue;
+                const uint32_t k = (uint32_t)__popcll(mk);
+                const uint32_t q = 64u / c;                       /* units of c per batch */
+                const uint32_t room = 64u - (T & 63u), f0 = room / c;   /* in the current batch */
+                const uint32_t nb = T + room;                     /* the next batch */
+                if (is_u && U_u == c) {
+                    const uint32_t i = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                    off_u = i < f0 ? T + c * i : nb + 64u * ((i - f0) / q) + c * ((i - f0) % q);
+                }
+                T = k <= f0 ? T + c * k : nb + 64u * ((k - f0 - 1u) / q) + c * ((k - f0 - 1u) % q + 1u);
             }
             const uint32_t sz = is_u ? ((n_u + 15u) & ~15u) : 0u;
             const uint32_t base = wave_scan(sz);
+            for (uint32_t p = lane; p < T; p += 64u) unit_of[p] = 0xffu;
+            wave_sync();
             if (is_u) {
                 L.u_off[wv][lane] = off_u;
                 L.u_base[wv][lane] = base - sz;           /* exclusive */
@@ -1569,29 +1661,42 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
         wave_sync();
         for (uint32_t b0 = 0; b0 < T; b0 += 64u) {
             const uint32_t p = b0 + lane;
-            const bool act = p < T;
-            const uint32_t u = act ? unit_of[p] : 0u;
-            const uint32_t un = L.u_n[wv][u], uU = gp_lanes(un);
+            const uint32_t uo = p < T ? (uint32_t)unit_of[p] : 0xffu;
+            const bool act = uo != 0xffu;
+            const uint32_t u = act ? uo : 0u;
+            const uint32_t un = L.u_n[wv][u], uU = gp_lanes(un), uP = gp_pow2(uU);
             const uint32_t site_l = u >> 1, smp = u & 1u;
             const uint32_t j = p - L.u_off[wv][u];
+            const uint32_t pb = L.u_off[wv][u] - b0;            /* the unit's first lane in this batch */
             LaneIn in;
-            const int rem = act ? (int)un - (int)(128u * j) : 0;
-            in.na = (uint32_t)min(max(rem, 0), 128);
-            in.na4 = (in.na + 3u) & ~3u;
-            in.nb = 0u;
-            in.nca = in.na4 >> 2;
-            asm("" : "+v"(in.nca));         /* as in ss_score_main */
-            in.nab = in.na4;
             const uint32_t *base_s = smp ? kernarg_args().reads_n : kernarg_args().reads_t;
-            const uint32_t start = act ? (smp ? L.c_on[wv][site_l] : L.c_ot[wv][site_l]) + 128u * j : 0u;
+            const uint32_t ustart = act ? (smp ? L.c_on[wv][site_l] : L.c_ot[wv][site_l]) : 0u;
+            /* the unit's reads in 4-read chunks dealt round-robin over its U
+             * lanes (lane j: chunks j, j + U, ..): one load instruction reads
+             * each unit's next 16 U bytes, contiguous across its lanes (any
+             * partition of a unit's reads sorts the same: the lanes merge).
+             * A lane loads only its unit's reads: chunks past its last load
+             * that one again (CLAMP), and a lane without reads loads the
+             * unit's first chunk, never another unit's reads */
+            const uint32_t cst = 4u * uU;
+            in.na = act && un > 4u * j ? un - 4u * j : 0u;
+            in.cstep = cst;
+            in.nca = LN_C;                  /* every chunk is A's (nb = 0) */
+            asm("" : "+v"(in.nca));
+            in.na4 = in.na;
+            in.nb = 0u;
+            in.nab = in.na;
+            const uint32_t start = ustart + (in.na ? 4u * j : 0u);
+            in.clast = in.na ? (in.na - 1u) / cst : 0u;
+            const uint32_t nch = wave_max(in.na ? in.clast + 1u : 0u);
+            const uint32_t last_w = in.clast * cst + 4u;     /* words past start the lane may load */
             in.pa = base_s + start;
             in.pb = in.pa;
             in.la = in.lb = 256u * (1u + smp * 16u + ((L.c_ref[wv][site_l] >> 8) & 0xffu));
-            const uint32_t nch = wave_max((in.nab + 3u) >> 2);
             const uint32_t endv = smp ? end_n : end_t;
-            in.tail = __ballot((uint64_t)start + 4u * nch > (uint64_t)endv) || end_t < 4u || end_n < 4u;
+            in.tail = __ballot((uint64_t)start + last_w > (uint64_t)endv) || end_t < 4u || end_n < 4u;
             uint32_t v[LN_R];
-            const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
+            const LaneAcc acc = ln_keys<true, true>(in, lut, nch, cap, v);
             /* the unit's counts before the sort: acc is not live across it */
             if (act) {
                 const uint32_t c = acc.cnt_a;
@@ -1601,10 +1706,10 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
                 if (acc.maxq >= 64u) ucnt[u][3] = 1u;     /* 8-bit records cannot hold its q */
             }
             ln_levels<LN_R, 2>(v);
-            if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }
-            if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }
-            if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }
-            if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }
+            if (__ballot(act && uP >= 2u)) { if (act && uP >= 2u) gp_level<2>(v, j, pb, uU); }
+            if (__ballot(act && uP >= 4u)) { if (act && uP >= 4u) gp_level<4>(v, j, pb, uU); }
+            if (__ballot(act && uP >= 8u)) { if (act && uP >= 8u) gp_level<8>(v, j, pb, uU); }
+            if (__ballot(act && uP >= 16u)) { if (act && uP >= 16u) gp_level<16>(v, j, pb, uU); }
             wave_sync();
             /* the unit's contributing keys as records, ascending, 16 per store:
              * past lim they stay inside the lane's 128 slots and the unit's

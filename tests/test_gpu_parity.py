@@ -115,12 +115,31 @@ def test_wide_sample_units_parity(pkg, oracle, lt, ln, fixed, n, wild, opts):
                                      (2040, 40, 20), (140, 3, 60), (2, 600, 40)])
 @pytest.mark.parametrize("opts", [OPTSETS[0], OPTSETS[-1]])
 def test_group_unit_boundaries(pkg, oracle, lt, ln, n, opts):
-    """Lane-group sort units (ss_score_group) at every lane-count boundary:
-    Poisson depths straddling 128 / 256 / 512 / 1024 / 2048 reads per sample,
-    so units of 1, 2, 4, 8 and 16 lanes (and the deep kernel past 2048) mix in
-    one batch of lanes, plus sites with a tiny or empty second sample."""
+    """Lane-group sort units (ss_score_group) at lane-count and network-size
+    boundaries: Poisson depths straddling 128 / 256 / 512 / 1024 / 2048 reads
+    per sample, so units of 1 .. 16 lanes (networks of 1, 2, 4, 8 and 16 lanes,
+    and the deep kernel past 2048) mix in one batch of lanes, plus sites with a
+    tiny or empty second sample."""
     batch = pkg.synth_batch_host(pkg.Synth.default(lt, ln, **EXOTIC), 11, n)
     assert_parity(pkg, oracle, batch, opts)
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_group_dense_unit_packing(pkg, oracle, seed):
+    """Units take ceil(n / 128) lanes (1 .. 16, not only powers of two) and are
+    packed by descending size into 64-lane batches, so a chunk mixes units of
+    3, 5, 6, 7, 9 .. 15 lanes whose virtual pad lanes belong to the next unit,
+    and batches end in empty lanes.  Depths spread over 129 .. 2048 reads per
+    sample, tumor and normal drawn independently, sites interleaved."""
+    import random
+    rnd = random.Random(seed)
+    lams = [(200, 700), (330, 1450), (650, 260), (900, 1180), (1150, 390), (1400, 1900), (1700, 540),
+            (1950, 1020)]
+    parts = [pkg.synth_batch_host(pkg.Synth.default(lt, ln, **EXOTIC), 30 + k, 9)
+             for k, (lt, ln) in enumerate(lams)]
+    sites = [b.site(i) for b in parts for i in range(b.n_sites)]
+    rnd.shuffle(sites)
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), OPTSETS[0])
 
 
 @pytest.mark.parametrize("n_group", [1, 31, 32, 33, 95])
