@@ -380,7 +380,7 @@ def site_bytes(lt: float, ln: float) -> float:
 # a context's own device memory (ss_capi.hip): the model tables (SS_TAB_BYTES)
 # and, at full-grid batches, the group kernel's fold-record buffers (n_CU x 12
 # waves x SS_GRP_REC_BYTES; allocated at the first batch that needs them)
-CTX_BYTES = 34_092_160 + 256 * 12 * (131072 + 128)
+CTX_BYTES = 34_092_416 + 256 * 12 * (131072 + 128)
 
 
 def c4_rank_bytes(scale: int, world: int, lt: float, ln: float, chunk: int):

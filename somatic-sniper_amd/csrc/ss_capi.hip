@@ -75,6 +75,8 @@ struct ss_ctx {
     /* device memory (dev_alloc): blocks in use, blocks outgrown but possibly still read */
     std::vector<dev_blk> *blocks, *retired;
     uint64_t fp_expect[3];    /* host fingerprint of the uploaded tables: coef, lhet, the rest */
+    uint8_t fast_thr[256];    /* SS_TAB_FAST (fast_table) */
+    int fast_ok;              /* SS_MF_FAST */
     int counted;              /* included in g_live */
 };
 
@@ -267,6 +269,35 @@ static void ctx_quiesce(ss_ctx_t *c)
     if (c->hstream) hipStreamSynchronize(c->hstream);
 }
 
+/* The main kernel's early exit (ss_kernels.hip ln_classify): for n = 1 .. 128
+ * reads per sample, the smallest count c24 of reads with minq >= 24 such that
+ *   24 * (fk[0] + .. + fk[c24 - 1]) * (1 - 1e-4) + min coef[q][n'][n'] >= 1
+ * over q in [4, 63] and n' in [1, n] (sniper_maqcns.c:184-196: the non-reference
+ * homozygotes' p when every read is on the reference); 255 = never.  The
+ * 1e-4 margin covers the float accumulation of esum (<= 128 roundings of
+ * 2^-24 relative each).  Enabled only with q_r >= 1, so a heterozygote never
+ * ties the reference homozygote in sniper_glf2cns. */
+static int fast_table(const ss_host_model_t &hm, uint8_t thr[256])
+{
+    memset(thr, 255, 256);
+    if (hm.q_r_int < 1) return 0;
+    double F[130];
+    F[0] = 0.0;
+    for (int k = 0; k < 129; ++k) F[k + 1] = F[k] + hm.fk[k < 255 ? k : 255];
+    double cm = 1e300;
+    int any = 0;
+    for (int n = 1; n <= 128; ++n) {
+        for (int q = 4; q < 64; ++q) cm = std::min(cm, hm.coef[(size_t)q << 16 | (size_t)n << 8 | (size_t)n]);
+        for (int c = 1; c <= n; ++c)
+            if (24.0 * F[c] * (1.0 - 1e-4) + cm >= 1.0) {
+                thr[n] = (uint8_t)c;
+                any = 1;
+                break;
+            }
+    }
+    return any;
+}
+
 /* fingerprint the context's device tables (ss_tab_fingerprint) and compare
  * with the host's sums; the caller's stream order puts this after the upload /
  * the launches it wants checked.  Synchronizes the context's stream. */
@@ -282,7 +313,7 @@ static int tables_verify(ss_ctx_t *c)
     if (fp[0] == c->fp_expect[0] && fp[1] == c->fp_expect[1] && fp[2] == c->fp_expect[2]) return SS_OK;
     fprintf(stderr, "[sniper_amd] device %d: the context's device tables no longer match the host's (%s%s%s differ)\n",
             c->device, fp[0] != c->fp_expect[0] ? "coef " : "", fp[1] != c->fp_expect[1] ? "lhet " : "",
-            fp[2] != c->fp_expect[2] ? "fk/qAdd/prior/nt16" : "");
+            fp[2] != c->fp_expect[2] ? "fk/qAdd/prior/nt16/fast" : "");
     return SS_E_TABLES;
 }
 
@@ -355,6 +386,7 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
         return SS_E_HIP;
     }
     hipStream_t hs = c->hstream;
+    c->fast_ok = fast_table(c->hm, c->fast_thr);
 #define TRY(x) do { if ((rc = (x)) != SS_OK) { ss_ctx_destroy(c); return rc; } } while (0)
     TRY(dev_alloc(c, (void **)&c->d_tab, SS_TAB_BYTES, hs));
     {
@@ -366,6 +398,7 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
             {SS_TAB_PRIOR, c->hm.prior, 160 * sizeof(int32_t)},
             {SS_TAB_JPRIOR, c->hm.jprior, 1600 * sizeof(int32_t)},
             {SS_TAB_NT16, ss_nt16_table, 256},
+            {SS_TAB_FAST, c->fast_thr, 256},
         };
         for (auto &pt : parts)
             if (hipMemcpyAsync(c->d_tab + pt.off, pt.src, pt.n, hipMemcpyHostToDevice, hs) != hipSuccess) {
@@ -531,7 +564,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     }
     a.m.min_somatic_qual = c->hm.prm.min_somatic_qual;
     a.m.flags = (c->hm.prm.use_joint_priors ? SS_MF_JOINT : 0u) | (c->hm.prm.include_loh ? SS_MF_LOH : 0u) |
-                (c->hm.prm.include_gor ? SS_MF_GOR : 0u);
+                (c->hm.prm.include_gor ? SS_MF_GOR : 0u) | (c->fast_ok ? SS_MF_FAST : 0u);
     const int deep_grid = c->n_cu * 3;              /* 3 blocks (12 one-site waves) per CU: LDS */
     c->last_stream = s;
     const hipEvent_t *evs = nullptr;

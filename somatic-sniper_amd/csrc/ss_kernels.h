@@ -19,11 +19,13 @@
 #define SS_TAB_PRIOR  (SS_TAB_QADD + (size_t)1024 * 4)            /* i32 [16 * 10]   */
 #define SS_TAB_JPRIOR (SS_TAB_PRIOR + (size_t)160 * 4)            /* i32 [16*10*10]  */
 #define SS_TAB_NT16   (SS_TAB_JPRIOR + (size_t)1600 * 4)          /* u8  [256]       */
-#define SS_TAB_BYTES  (SS_TAB_NT16 + (size_t)256)
+#define SS_TAB_FAST   (SS_TAB_NT16 + (size_t)256)                 /* u8  [256]: the early exit's c24 per depth */
+#define SS_TAB_BYTES  (SS_TAB_FAST + (size_t)256)
 
 #define SS_MF_JOINT 1u
 #define SS_MF_LOH   2u
 #define SS_MF_GOR   4u
+#define SS_MF_FAST  8u   /* SS_TAB_FAST is valid (q_r >= 1): the main kernel's early exit may run */
 
 struct ss_dev_model {
     const uint8_t *tab;      /* SS_TAB_* layout */
@@ -45,6 +47,7 @@ SS_TAB_ACCESSOR(qadd, int32_t, SS_TAB_QADD)
 SS_TAB_ACCESSOR(prior, int32_t, SS_TAB_PRIOR)
 SS_TAB_ACCESSOR(jprior, int32_t, SS_TAB_JPRIOR)
 SS_TAB_ACCESSOR(nt16, uint8_t, SS_TAB_NT16)
+SS_TAB_ACCESSOR(fast, uint8_t, SS_TAB_FAST)
 #undef SS_TAB_ACCESSOR
 
 /* Per-launch arguments of the scoring kernels. */

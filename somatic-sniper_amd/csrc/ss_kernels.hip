@@ -807,6 +807,9 @@ namespace {
 #define LN_C (LN_N / 4)              /* 4-element chunks (one x4 load each)       */
 #define LN_P 4                       /* chunk loads in flight ahead of the key build */
 #define LN_WAVES (SS_MAIN_BLOCK / 64)
+#ifndef SS_EARLY_MAX_READS
+#define SS_EARLY_MAX_READS 72u       /* blocks of at most this mean (tumor + normal) reads per site take the early exit */
+#endif
 
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
@@ -892,8 +895,18 @@ __device__ __forceinline__ uint32_t ln_elem(const uint32_t (&v)[R], int e)
  * read's group count increment (1 << 8 * base).  Entry 0 belongs to a
  * non-contributing read (clamped q = 0, or a pad): key 0xffff, no count.  Row
  * (sample, ref16) starts at byte 256 * (1 + sample * 16 + ref16) and a read
- * indexes it by (nt16 | strand << 4) * 8 = (read >> 13) & 0xf8. */
+ * indexes it by (nt16 | strand << 4) * 8 = (read >> 13) & 0xf8, XOR-swizzled
+ * by the row (ln_lut_row). */
 #define LN_LUT_BYTES (256 * (1 + 2 * 16))
+
+/* Rows are 256 B, i.e. exactly the 64 LDS banks, so the same entry of two rows
+ * would sit in the same banks and lanes of different references / samples
+ * reading it would conflict: entry k of row r is stored at k ^ (r & 31), and a
+ * read's offset is (read >> 13 & 0xf8) ^ ln_lut_row(r) (one v_bitop3). */
+__device__ __forceinline__ uint32_t ln_lut_row(uint32_t r)
+{
+    return 256u * r | (r & 31u) << 3;
+}
 
 __device__ __forceinline__ void ln_lut_build(uint2 *lut)
 {
@@ -903,7 +916,7 @@ __device__ __forceinline__ void ln_lut_build(uint2 *lut)
         const uint32_t code = nt16 ? nt16 : ref16;
         const uint32_t nt4 = code == 1u ? 0u : code == 2u ? 1u : code == 4u ? 2u : code == 8u ? 3u : 4u;
         const uint32_t hb = nt4 < 4u ? 1u : 0u, base = hb ? nt4 : 0u;
-        lut[i] = rw == 0u ? make_uint2(0xffffu, 0u)
+        lut[(rw << 5) | ((i ^ rw) & 31u)] = rw == 0u ? make_uint2(0xffffu, 0u)
                           : make_uint2(smp << 15 | base << 13 | hb << 4 | st << 3, 1u << (8u * base));
     }
 }
@@ -921,7 +934,7 @@ struct LaneIn {
     const uint32_t *pa, *pb;         /* element e's read: pa + e (e < na4), pb + e (e >= na4) */
     uint32_t na, nb, na4;
     uint32_t nca, nab;               /* A's chunks (na4 / 4); na4 + nb */
-    uint32_t la, lb;                 /* byte offsets of A's and B's lookup rows (see LN_LUT_BYTES) */
+    uint32_t la, lb;                 /* A's and B's lookup rows (ln_lut_row) */
     uint32_t clast;                  /* CLAMP loads: chunks past this one load it again */
     uint32_t cstep;                  /* STRIDE: words from one chunk of the lane to its next */
     bool tail;                       /* wave-uniform: an x4 load could pass the end of the reads */
@@ -992,7 +1005,7 @@ __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint2 *lut, uin
         lo6[t] = rd[t] & 0x3f00u;
         y[t] = rd[t] >> 13;
         /* contributing unless the clamped q is 0 (sniper_maqcns.c:165-167) */
-        const uint32_t off = __umul24((y[t] & 0xf8u) | row, ln_nz(minq[t] | lo6[t]));
+        const uint32_t off = __umul24((y[t] & 0xf8u) ^ row, ln_nz(minq[t] | lo6[t]));
         ent[t] = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(lut) + off);
     }
     uint32_t crms = 0, ccnt = 0;
@@ -1298,6 +1311,236 @@ __device__ __forceinline__ const ss_score_args &kernarg_args()
     return *(const ss_score_args *)p;
 }
 
+/* The lane path for one block of 64 sites, lane = site s (insite: a real
+ * site): key build, sort, records, fold, likelihoods, decision; sites it does
+ * not score are appended to the wave's segment of the group kernel's list
+ * (ndeep: entries so far). */
+__device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, bool insite, const uint2 *lut,
+                                         const double *fk, const int16_t *qtab, LaneLds &L, uint32_t lane,
+                                         uint32_t gw, uint32_t cap, uint32_t end_t, uint32_t end_n,
+                                         uint32_t &ndeep)
+{
+    uint32_t ot = 0, ot1 = 0, on = 0, on1 = 0, refc = 'N';
+    if (insite) {
+        ot = a.off_t[s];
+        ot1 = a.off_t[s + 1];
+        on = a.off_n[s];
+        on1 = a.off_n[s + 1];
+        refc = a.ref[s];
+    }
+    const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
+    const uint32_t nt = ot1 - ot, nn = on1 - on;
+    const bool formed = ot <= ot1 && ot1 <= end_t && on <= on1 && on1 <= end_n;
+    bool ok = insite && formed && nt <= LN_N && nn <= LN_N;
+    const uint32_t nt4 = (nt + 3u) & ~3u, nn4 = (nn + 3u) & ~3u;
+    /* wave-uniform shape: joint when every ok site fits one network */
+    /* a block whose x4 loads could pass the end of the batch's reads (its
+     * last sites) loads word by word; so does a batch of fewer than 4
+     * tumor reads (the x4 loads of read-less chunks go to reads_t[0..3]) */
+    const bool tail = __ballot(ok && (ot + nt4 > end_t || on + nn4 > end_n)) || end_t < 4u;
+    const bool joint = !__ballot(ok && nt4 + nn > LN_N);
+    bool wild = false;
+    uint32_t lkN03 = 0, lkN47 = 0, lkN89 = 0, cnsN = 0, mqN = 0;
+    /* joint: one pass, both samples; separate: the tumor, then the normal */
+    for (uint32_t pass = 0; pass < (joint ? 1u : 2u); ++pass) {
+        LaneIn in;
+        const bool nrm = pass == 1u;
+        in.na = ok ? (nrm ? nn : nt) : 0u;
+        in.na4 = ok ? (nrm ? nn4 : nt4) : 0u;
+        in.nb = joint && ok ? nn : 0u;
+        in.nca = in.na4 >> 2;
+        /* opaque: otherwise the chunk tests c < nca become 4c < na4, whose
+         * constants 68 .. 124 are not inline and took 16 SGPRs */
+        asm("" : "+v"(in.nca));
+        in.nab = in.na4 + in.nb;
+        const uint32_t ob = ok ? on : 0u;
+        in.pa = (nrm ? a.reads_n : a.reads_t) + (ok ? (nrm ? on : ot) : 0u);
+        in.pb = a.reads_n + ob - in.na4;
+        in.la = ln_lut_row(1u + (nrm ? 16u : 0u) + ref16);
+        in.lb = ln_lut_row(17u + ref16);
+        const uint32_t nch = wave_max((in.nab + 3u) >> 2);
+        /* chunks past A's reads load from pb: up to ob - na4 + 4 nch */
+        in.tail = tail || __ballot((uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4);
+        uint32_t v[LN_R];
+        const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
+        /* a read of minq >= 64 needs 16-bit records: the site goes to the group kernel */
+        wild = wild || acc.maxq >= 64u;
+        ln_levels<LN_R, 2>(v);
+        ln_records(v, 4u * nch, L, lane);
+        /* fold and finish the pass's samples: A (its records from 0), then
+         * in joint mode B (after A's contributing reads) */
+        const uint32_t ca = acc.cnt_a;
+        const uint32_t tot_a = (ca & 0xffu) + (ca >> 8 & 0xffu) + (ca >> 16 & 0xffu) + (ca >> 24);
+        for (uint32_t k = 0; k < (joint ? 2u : 1u); ++k) {
+            const bool smpN = nrm || k == 1u;
+            float es[4], fs[4];
+            uint32_t c[4];
+            ln_fold(L, lane, k ? tot_a : 0u, k ? acc.cnt_b : acc.cnt_a, fk, es, fs, c);
+            uint32_t l03, l47, l89, cn, mq;
+            ln_finish(es, fs, c, smpN ? nn : nt, k ? acc.rms_b : acc.rms_a, a.m, l03, l47, l89, cn, mq);
+            if (smpN) {
+                lkN03 = l03; lkN47 = l47; lkN89 = l89; cnsN = cn; mqN = mq;
+            } else {
+                L.tres[0][lane] = l03; L.tres[1][lane] = l47; L.tres[2][lane] = l89;
+                L.tres[3][lane] = cn;  L.tres[4][lane] = mq;
+            }
+        }
+        wave_sync();                                     /* the pass's records are read */
+    }
+    ok = ok && !wild;
+    /* sites the lane path does not score: the group kernel's list (one
+     * segment per wave, no atomics) */
+    const uint64_t out = __ballot(insite && !ok);
+    if (out) {
+        if (insite && !ok) {
+            const uint32_t d = ndeep + __builtin_amdgcn_mbcnt_hi((uint32_t)(out >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)out, 0u));
+            const ss_score_args &k = kernarg_args();
+            if (d < k.deep_seg_cap) k.deep_list[(size_t)gw * k.deep_seg_cap + d] = s;
+            else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
+        }
+        ndeep += (uint32_t)__popcll(out);
+    }
+    if (!formed && insite) atomicOr(kernarg_args().err, SS_KERR_MALFORMED);
+    const uint32_t dt = nt > 16777215u ? 16777215u : nt, dn = nn > 16777215u ? 16777215u : nn;
+    const uint32_t lkT03 = L.tres[0][lane], lkT47 = L.tres[1][lane], lkT89 = L.tres[2][lane];
+    const uint32_t cnsT = L.tres[3][lane], mqT = L.tres[4][lane];
+    wave_sync();                                         /* res overlays the records */
+    if (ok) {
+        ln_store_res(L.res[lane][0], lkT03, lkT47, lkT89, cnsT, dt, mqT);
+        ln_store_res(L.res[lane][1], lkN03, lkN47, lkN89, cnsN, dn, mqN);
+        ss_glf_t *glf = kernarg_args().glf;
+        if (glf) {
+            ln_store_glf(&glf[2ull * s], ref16, lkT03, lkT47, lkT89, mqT, dt);
+            ln_store_glf(&glf[2ull * s + 1], ref16, lkN03, lkN47, lkN89, mqN, dn);
+        }
+    }
+    wave_sync();
+    if (ok) decide_site(kernarg_args(), qtab, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
+    wave_sync();
+}
+
+/* Early exit of the lane path (round 5), for shallow blocks:
+ * before any key is built, a count pass over a site's reads decides the sites
+ * whose result needs no likelihood at all and writes their score; the others
+ * are queued for ln_block.  Exact -- the reference's own outcome -- and never
+ * taken when glf records are requested:
+ *   - ref char 'N' or an empty sample: -1 (somatic_sniper.c:127);
+ *   - a reference code of 15 other than 'N' ('n', ...): 255, never an SNV
+ *     candidate (:156);
+ *   - reference A/C/G/T, every read of both samples on the reference base
+ *     (bam_nt16_nt4_table semantics, sniper_maqcns.c:153-154: N/IUPAC reads
+ *     count as A, '=' as the reference) and enough reads of minq >= 24: 255.
+ *     Then in each sample the reference homozygote has p = 0 (tmp2 = 0,
+ *     :196) and every other homozygote p = esum + coef[bar_e][n][n] with
+ *     esum >= 24 * (fk[0] + .. + fk[c24 - 1]) (the walk visits the c24 reads
+ *     of q >= 24 first, each with a weight fk[w] >= fk[k]); the host table
+ *     SS_TAB_FAST holds, per read count n, the smallest c24 that makes that
+ *     >= 1 for every bar_e and every n' <= n (ss_capi.hip fast_table), so
+ *     those homozygotes quantise to lk >= 1, the heterozygotes score
+ *     >= q_r >= 1 (SS_MF_FAST requires it), and sniper_glf2cns (:250-273)
+ *     calls the reference homozygote in both samples: no candidate.
+ * Returns true when it wrote the site's score. */
+__device__ __forceinline__ void ln_count_chunk(const LaneIn &in, const uint2 *lut, uint32_t c, const uint32_t (&x)[4],
+                                               uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24)
+{
+    const bool fa = c < in.nca;
+    const int lim = (int)(fa ? in.na : in.nab) - (int)(4u * c);
+    uint32_t valid, vl;
+    asm("v_med3_i32 %0, %1, 0, 4" : "=v"(vl) : "v"(lim));
+    asm("v_bfm_b32 %0, %1, 0" : "=v"(valid) : "v"(vl));
+    const uint32_t row = fa ? in.la : in.lb;
+    uint32_t cc = 0, q = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        uint32_t vm;
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(vm) : "v"(valid), "i"(t));
+        const uint32_t rd = x[t] & vm;
+        /* every read counts, contributing or not; a masked element reads entry 0 (no count) */
+        const uint32_t off = (((rd >> 13) & 0xf8u) ^ row) & vm;
+        cc += reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lut) + off)[1];
+        uint32_t minq;
+        asm("v_min_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_1"
+            : "=v"(minq) : "v"(rd));
+        q += minq >= 24u ? 1u : 0u;
+    }
+    cnt_t += cc;
+    cnt_a += fa ? cc : 0u;
+    c24 += fa ? q : q << 16;
+}
+
+__device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 *lut, uint32_t s, bool insite,
+                                            uint32_t end_t, uint32_t end_n)
+{
+    uint32_t ot = 0, ot1 = 0, on = 0, on1 = 0, refc = 'N';
+    if (insite) {
+        ot = a.off_t[s];
+        ot1 = a.off_t[s + 1];
+        on = a.off_n[s];
+        on1 = a.off_n[s + 1];
+        refc = a.ref[s];
+    }
+    const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
+    const uint32_t nt = ot1 - ot, nn = on1 - on;
+    const bool small = insite && ot <= ot1 && ot1 <= end_t && on <= on1 && on1 <= end_n && nt <= LN_N && nn <= LN_N;
+    bool done = false;
+    int32_t sc = 255;
+    if (small && (refc == 'N' || nt == 0u || nn == 0u)) {
+        done = true;
+        sc = -1;
+    } else if (small && ref16 == 15u) {
+        done = true;
+    }
+    const bool acgt = ref16 == 1u || ref16 == 2u || ref16 == 4u || ref16 == 8u;
+    const bool cand = small && !done && acgt;
+    if (__ballot(cand)) {
+        LaneIn in;
+        in.na = cand ? nt : 0u;
+        in.na4 = (in.na + 3u) & ~3u;
+        in.nb = cand ? nn : 0u;
+        in.nca = in.na4 >> 2;
+        asm("" : "+v"(in.nca));
+        in.nab = in.na4 + in.nb;
+        const uint32_t oa = cand ? ot : 0u, ob = cand ? on : 0u;
+        in.pa = a.reads_t + oa;
+        in.pb = a.reads_n + ob - in.na4;
+        in.la = ln_lut_row(1u + ref16);
+        in.lb = ln_lut_row(17u + ref16);
+        const uint32_t nch = wave_max((in.nab + 3u) >> 2);
+        /* as in ln_block: word loads when an x4 load could pass the end of the reads */
+        in.tail = __ballot((uint64_t)oa + in.na4 > (uint64_t)end_t ||
+                           (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4) ||
+                  end_t < 4u || end_n < 4u;
+        uint32_t cnt_a = 0, cnt_t = 0, c24 = 0;
+        /* groups of LN_P chunk loads in flight, as in ln_keys */
+        uint32_t buf[2][LN_P][4];
+        if (nch > 0u) {
+#pragma unroll
+            for (int j = 0; j < LN_P; ++j) ln_load<false, false>(in, (uint32_t)j, buf[0][j]);
+        }
+#pragma unroll
+        for (int g = 0; g < LN_C / LN_P; ++g) {
+            if ((uint32_t)(g * LN_P) >= nch) break;
+            if (g + 1 < LN_C / LN_P && (uint32_t)((g + 1) * LN_P) < nch) {
+#pragma unroll
+                for (int j = 0; j < LN_P; ++j) ln_load<false, false>(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
+            }
+#pragma unroll
+            for (int j = 0; j < LN_P; ++j) ln_count_chunk(in, lut, (uint32_t)(g * LN_P + j), buf[g & 1][j], cnt_a, cnt_t, c24);
+        }
+        const uint32_t sh = 8u * (uint32_t)__builtin_ctz(ref16 | 16u);   /* the reference base's count field */
+        const uint32_t cnt_b = cnt_t - cnt_a;
+        const uint32_t tot_a = (cnt_a & 0xffu) + (cnt_a >> 8 & 0xffu) + (cnt_a >> 16 & 0xffu) + (cnt_a >> 24);
+        const uint32_t tot_b = (cnt_b & 0xffu) + (cnt_b >> 8 & 0xffu) + (cnt_b >> 16 & 0xffu) + (cnt_b >> 24);
+        if (cand && tot_a == nt && tot_b == nn && ((cnt_a >> sh) & 0xffu) == nt && ((cnt_b >> sh) & 0xffu) == nn) {
+            const uint8_t *thr = ss_tab_fast(a.m);
+            if ((c24 & 0xffffu) >= thr[nt] && (c24 >> 16) >= thr[nn]) done = true;
+        }
+    }
+    if (done) kernarg_args().score[s] = sc;
+    return done;
+}
+
 /* compiled for 3 waves per SIMD: the per-lane network's 64 registers, the
  * chunk loads in flight and the key arithmetic need about 160 VGPRs (at 128
  * the compiler spills); the records take 8 KB of LDS per wave */
@@ -1310,6 +1553,7 @@ void ss_score_main(ss_score_args a)
     /* qAddTable (somatic_sniper.c:13,101-107) in LDS as int16 (its entries lie
      * in [-512, 0]; 2 KB keeps 3 workgroups per CU within 160 KB) */
     __shared__ int16_t qtab[1024];
+    __shared__ uint16_t qq[LN_WAVES][128];          /* the early exit's queue: 63 carried + 64 new sites */
     for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < 256u ? ss_tab_fk(a.m)[i] : 0.0;
     for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) qtab[i] = (int16_t)ss_tab_qadd(a.m)[i];
     ln_lut_build(lut);
@@ -1324,107 +1568,68 @@ void ss_score_main(ss_score_args a)
     const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
     const uint32_t gw = blockIdx.x * LN_WAVES + wv;
     uint32_t ndeep = 0;
-    for (uint32_t blk = gw; blk < nblocks; blk += nwaves) {
-        const uint32_t s = blk * 64u + lane;
-        const bool insite = s < n_sites;
-        uint32_t ot = 0, ot1 = 0, on = 0, on1 = 0, refc = 'N';
-        if (insite) {
-            ot = a.off_t[s];
-            ot1 = a.off_t[s + 1];
-            on = a.off_n[s];
-            on1 = a.off_n[s + 1];
-            refc = a.ref[s];
-        }
-        const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
-        const uint32_t nt = ot1 - ot, nn = on1 - on;
-        const bool formed = ot <= ot1 && ot1 <= end_t && on <= on1 && on1 <= end_n;
-        bool ok = insite && formed && nt <= LN_N && nn <= LN_N;
-        const uint32_t nt4 = (nt + 3u) & ~3u, nn4 = (nn + 3u) & ~3u;
-        /* wave-uniform shape: joint when every ok site fits one network */
-        /* a block whose x4 loads could pass the end of the batch's reads (its
-         * last sites) loads word by word; so does a batch of fewer than 4
-         * tumor reads (the x4 loads of read-less chunks go to reads_t[0..3]) */
-        const bool tail = __ballot(ok && (ot + nt4 > end_t || on + nn4 > end_n)) || end_t < 4u;
-        const bool joint = !__ballot(ok && nt4 + nn > LN_N);
-        bool wild = false;
-        uint32_t lkN03 = 0, lkN47 = 0, lkN89 = 0, cnsN = 0, mqN = 0;
-        /* joint: one pass, both samples; separate: the tumor, then the normal */
-        for (uint32_t pass = 0; pass < (joint ? 1u : 2u); ++pass) {
-            LaneIn in;
-            const bool nrm = pass == 1u;
-            in.na = ok ? (nrm ? nn : nt) : 0u;
-            in.na4 = ok ? (nrm ? nn4 : nt4) : 0u;
-            in.nb = joint && ok ? nn : 0u;
-            in.nca = in.na4 >> 2;
-            /* opaque: otherwise the chunk tests c < nca become 4c < na4, whose
-             * constants 68 .. 124 are not inline and took 16 SGPRs */
-            asm("" : "+v"(in.nca));
-            in.nab = in.na4 + in.nb;
-            const uint32_t ob = ok ? on : 0u;
-            in.pa = (nrm ? a.reads_n : a.reads_t) + (ok ? (nrm ? on : ot) : 0u);
-            in.pb = a.reads_n + ob - in.na4;
-            in.la = 256u * (1u + (nrm ? 16u : 0u) + ref16);
-            in.lb = 256u * (17u + ref16);
-            const uint32_t nch = wave_max((in.nab + 3u) >> 2);
-            /* chunks past A's reads load from pb: up to ob - na4 + 4 nch */
-            in.tail = tail || __ballot((uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4);
-            uint32_t v[LN_R];
-            const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
-            /* a read of minq >= 64 needs 16-bit records: the site goes to the group kernel */
-            wild = wild || acc.maxq >= 64u;
-            ln_levels<LN_R, 2>(v);
-            ln_records(v, 4u * nch, L, lane);
-            /* fold and finish the pass's samples: A (its records from 0), then
-             * in joint mode B (after A's contributing reads) */
-            const uint32_t ca = acc.cnt_a;
-            const uint32_t tot_a = (ca & 0xffu) + (ca >> 8 & 0xffu) + (ca >> 16 & 0xffu) + (ca >> 24);
-            for (uint32_t k = 0; k < (joint ? 2u : 1u); ++k) {
-                const bool smpN = nrm || k == 1u;
-                float es[4], fs[4];
-                uint32_t c[4];
-                ln_fold(L, lane, k ? tot_a : 0u, k ? acc.cnt_b : acc.cnt_a, fk, es, fs, c);
-                uint32_t l03, l47, l89, cn, mq;
-                ln_finish(es, fs, c, smpN ? nn : nt, k ? acc.rms_b : acc.rms_a, a.m, l03, l47, l89, cn, mq);
-                if (smpN) {
-                    lkN03 = l03; lkN47 = l47; lkN89 = l89; cnsN = cn; mqN = mq;
-                } else {
-                    L.tres[0][lane] = l03; L.tres[1][lane] = l47; L.tres[2][lane] = l89;
-                    L.tres[3][lane] = cn;  L.tres[4][lane] = mq;
+    /* the early exit (ln_classify) needs no glf output and the host's table;
+     * the sites it does not decide wait in the wave's queue (LDS entries
+     * k << 6 | lane: the wave's k-th block) and are scored 64 at a time by
+     * ln_block, so its lanes stay full */
+    /* a batch whose mean depth is well past the blocks' threshold (C4's 89
+     * reads per site) never looks at its blocks' depths */
+    const uint64_t all_reads = (uint64_t)(end_t - a.off_t[0]) + (end_n - a.off_n[0]);
+    const bool early = a.glf == nullptr && (a.m.flags & SS_MF_FAST) != 0u &&
+                       all_reads <= (uint64_t)(SS_EARLY_MAX_READS + 8u) * n_sites;
+    uint16_t *queue = qq[wv];
+    uint32_t qn = 0;                                          /* wave-uniform */
+    uint32_t k = 0, blk = gw;
+    /* one ln_block call site (three of them spilled): each iteration scores a
+     * block directly, or classifies a shallow one and scores a full queue
+     * batch, or at the end the queue's last, partial batch */
+    for (;;) {
+        uint32_t s = 0;
+        bool insite = false, run = true;
+        if (blk < nblocks) {
+            s = blk * 64u + lane;
+            insite = s < n_sites;
+            /* only shallow blocks take the exit: at 30x/30x it pays, at 60x/30x
+             * the count pass and the queued sites' second load cost more than
+             * the skipped work; the block's reads from its
+             * offsets (scalar loads) */
+            bool shallow = false;
+            if (early && k < 1024u) {                         /* (queue entries hold k < 1024) */
+                const uint32_t s0 = blk * 64u, s1 = min(s0 + 64u, n_sites);
+                const uint32_t breads = (a.off_t[s1] - a.off_t[s0]) + (a.off_n[s1] - a.off_n[s0]);
+                shallow = breads <= SS_EARLY_MAX_READS * (s1 - s0);
+            }
+            if (shallow) {
+                const bool need = insite && !ln_classify(kernarg_args(), lut, s, insite, end_t, end_n);
+                const uint64_t m = __ballot(need);
+                if (need)
+                    queue[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                        (uint16_t)(k << 6 | lane);
+                qn += (uint32_t)__popcll(m);
+                run = qn >= 64u;
+                if (run) {                                    /* a full batch of queued sites */
+                    qn -= 64u;
+                    wave_sync();
+                    const uint32_t e = queue[qn + lane];
+                    wave_sync();
+                    s = (gw + (e >> 6) * nwaves) * 64u + (e & 63u);
+                    insite = true;
                 }
             }
-            wave_sync();                                     /* the pass's records are read */
+            blk += nwaves;
+            ++k;
+        } else if (qn) {                                      /* the wave's last, partial batch */
+            wave_sync();
+            const uint32_t e = lane < qn ? (uint32_t)queue[lane] : 0u;
+            wave_sync();
+            s = (gw + (e >> 6) * nwaves) * 64u + (e & 63u);
+            insite = lane < qn;
+            qn = 0;
+        } else {
+            break;
         }
-        ok = ok && !wild;
-        /* sites the lane path does not score: the group kernel's list (one
-         * segment per wave, no atomics) */
-        const uint64_t out = __ballot(insite && !ok);
-        if (out) {
-            if (insite && !ok) {
-                const uint32_t d = ndeep + __builtin_amdgcn_mbcnt_hi((uint32_t)(out >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)out, 0u));
-                const ss_score_args &k = kernarg_args();
-                if (d < k.deep_seg_cap) k.deep_list[(size_t)gw * k.deep_seg_cap + d] = s;
-                else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
-            }
-            ndeep += (uint32_t)__popcll(out);
-        }
-        if (!formed && insite) atomicOr(kernarg_args().err, SS_KERR_MALFORMED);
-        const uint32_t dt = nt > 16777215u ? 16777215u : nt, dn = nn > 16777215u ? 16777215u : nn;
-        const uint32_t lkT03 = L.tres[0][lane], lkT47 = L.tres[1][lane], lkT89 = L.tres[2][lane];
-        const uint32_t cnsT = L.tres[3][lane], mqT = L.tres[4][lane];
-        wave_sync();                                         /* res overlays the records */
-        if (ok) {
-            ln_store_res(L.res[lane][0], lkT03, lkT47, lkT89, cnsT, dt, mqT);
-            ln_store_res(L.res[lane][1], lkN03, lkN47, lkN89, cnsN, dn, mqN);
-            ss_glf_t *glf = kernarg_args().glf;
-            if (glf) {
-                ln_store_glf(&glf[2ull * s], ref16, lkT03, lkT47, lkT89, mqT, dt);
-                ln_store_glf(&glf[2ull * s + 1], ref16, lkN03, lkN47, lkN89, mqN, dn);
-            }
-        }
-        wave_sync();
-        if (ok) decide_site(kernarg_args(), qtab, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);
-        wave_sync();
+        if (run) ln_block(kernarg_args(), s, insite, lut, fk, qtab, L, lane, gw, cap, end_t, end_n, ndeep);
     }
     if (lane == 0 && ndeep) {
         /* one atomic numbers the segment and places its entries, so the
@@ -1692,7 +1897,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
             const uint32_t last_w = in.clast * cst + 4u;     /* words past start the lane may load */
             in.pa = base_s + start;
             in.pb = in.pa;
-            in.la = in.lb = 256u * (1u + smp * 16u + ((L.c_ref[wv][site_l] >> 8) & 0xffu));
+            in.la = in.lb = ln_lut_row(1u + smp * 16u + ((L.c_ref[wv][site_l] >> 8) & 0xffu));
             const uint32_t endv = smp ? end_n : end_t;
             in.tail = __ballot((uint64_t)start + last_w > (uint64_t)endv) || end_t < 4u || end_n < 4u;
             uint32_t v[LN_R];

@@ -432,12 +432,32 @@ def all_reference_sites(pkg):
 @pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"]])
 def test_all_reference_sites_parity(pkg, oracle, opts):
     """all_reference_sites against the oracle, with and without glf records,
-    plus a 60x/30x batch with few errors (most sites all-reference)."""
+    plus 60x/30x and 30x/25x batches with few errors (most sites
+    all-reference; the shallow one takes the main kernel's early exit when
+    scored without glf)."""
     batch = pkg.Batch.from_sites(all_reference_sites(pkg))
     assert_parity(pkg, oracle, batch, opts)
-    clean = pkg.synth_batch_host(pkg.Synth.default(60, 30, seed=77, p_error=0.002, p_nbase=0.0005,
-                                                   p_somatic=0.01, p_germline=0.01), 0, 20000)
-    assert_parity(pkg, oracle, clean, opts)
+    for lt, ln in ((60, 30), (30, 25)):
+        clean = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=77, p_error=0.002, p_nbase=0.0005,
+                                                       p_somatic=0.01, p_germline=0.01), 0, 20000)
+        assert_parity(pkg, oracle, clean, opts)
+
+
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"]])
+def test_early_exit_mixed_blocks(pkg, oracle, opts):
+    """The main kernel's early exit is decided per 64-site block (mean depth
+    <= 72 reads per site, in a batch of mean <= 80): shallow blocks (25x/20x)
+    and deep ones (60x/45x) alternate, so the undecided sites of shallow
+    blocks wait in the wave's queue while deep blocks are scored directly,
+    and the queue's last, partial batch is scored at the end."""
+    sh = pkg.synth_batch_host(pkg.Synth.default(25, 20, seed=91, **EXOTIC), 0, 64 * 40)
+    dp = pkg.synth_batch_host(pkg.Synth.default(60, 45, seed=92, **EXOTIC), 0, 64 * 40 + 17)
+    sites = []
+    for b in range(40):
+        sites += [sh.site(64 * b + i) for i in range(64)]
+        sites += [dp.site(64 * b + i) for i in range(64)]
+    sites += [dp.site(64 * 40 + i) for i in range(17)]
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), opts)
 
 
 @pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"]])

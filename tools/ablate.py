@@ -47,20 +47,20 @@ EDITS = {
                 "    if (true) {\n#pragma unroll\n        for (int t = 0; t < 4; ++t) "
                 "x[t] = ((in.na + 4u * c + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;\n        return;\n    }\n"
                 "    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */\n")],
-    "gnosort": [("            ln_levels<LN_R, 2>(v);\n            if (__ballot(act && uU >= 2u))",
-                 "            if (__ballot(act && uU >= 2u))")],
-    "gnomerge": [("            if (__ballot(act && uU >= 2u)) { if (act && uU >= 2u) gp_level<2>(v, j); }\n"
-                  "            if (__ballot(act && uU >= 4u)) { if (act && uU >= 4u) gp_level<4>(v, j); }\n"
-                  "            if (__ballot(act && uU >= 8u)) { if (act && uU >= 8u) gp_level<8>(v, j); }\n"
-                  "            if (__ballot(act && uU >= 16u)) { if (act && uU >= 16u) gp_level<16>(v, j); }\n", "")],
+    "gnosort": [("            ln_levels<LN_R, 2>(v);\n            if (__ballot(act && uP >= 2u))",
+                 "            if (__ballot(act && uP >= 2u))")],
+    "gnomerge": [("            if (__ballot(act && uP >= 2u)) { if (act && uP >= 2u) gp_level<2>(v, j, pb, uU); }\n"
+                  "            if (__ballot(act && uP >= 4u)) { if (act && uP >= 4u) gp_level<4>(v, j, pb, uU); }\n"
+                  "            if (__ballot(act && uP >= 8u)) { if (act && uP >= 8u) gp_level<8>(v, j, pb, uU); }\n"
+                  "            if (__ballot(act && uP >= 16u)) { if (act && uP >= 16u) gp_level<16>(v, j, pb, uU); }\n", "")],
     "gnorec": [("                    *reinterpret_cast<uint4 *>(gbuf + ubase + 4u * (uint32_t)i) =\n"
                 "                        make_uint4(ln_rec_dword(v, i), ln_rec_dword(v, i + 1), ln_rec_dword(v, i + 2),\n"
                 "                                   ln_rec_dword(v, i + 3));\n",
                 "                    asm volatile(\"\" :: \"v\"(ubase));\n")],
     "gnofold": [("        fold_sample(recs, m3.rec_n & 0x1ffffu, cnt, fk, es, fs);\n",
                  "        for (int b = 0; b < 4; ++b) es[b] = fs[b] = (float)cnt[b] + (float)(m3.rec_n >> b);\n")],
-    "gnofin": [("    geno_p5(role, es, fs, c, tot, a.m, mine);\n",
-                "    for (int t = 0; t < 5; ++t) mine[t] = es[t & 3] + (float)c[t & 3];\n")],
+    "gnofin": [("    geno_p5(0u, es, fs, c, tot, a.m, p);\n    geno_p5(1u, es, fs, c, tot, a.m, p + 5);\n",
+                "    for (int t = 0; t < 10; ++t) p[t] = es[t & 3] + (float)c[t & 3];\n")],
 }
 
 
