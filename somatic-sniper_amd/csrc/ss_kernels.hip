@@ -1353,14 +1353,20 @@ __device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, boo
          * constants 68 .. 124 are not inline and took 16 SGPRs */
         asm("" : "+v"(in.nca));
         in.nab = in.na4 + in.nb;
-        const uint32_t ob = ok ? on : 0u;
-        in.pa = (nrm ? a.reads_n : a.reads_t) + (ok ? (nrm ? on : ot) : 0u);
-        in.pb = a.reads_n + ob - in.na4;
+        const uint32_t ob = ok ? on : 0u, oa = ok ? (nrm ? on : ot) : 0u;
+        in.pa = (nrm ? a.reads_n : a.reads_t) + oa;
+        /* chunks past A's reads: joint mode, the normal's reads; a pass of one
+         * sample (no B part), the reads after A's in the same array -- the
+         * next sites', which their lanes load anyway (the tumor pass used to
+         * read the normal's reads here, loaded again by the normal pass) */
+        const bool solo = !joint;
+        in.pb = solo ? in.pa : a.reads_n + ob - in.na4;
         in.la = ln_lut_row(1u + (nrm ? 16u : 0u) + ref16);
         in.lb = ln_lut_row(17u + ref16);
         const uint32_t nch = wave_max((in.nab + 3u) >> 2);
-        /* chunks past A's reads load from pb: up to ob - na4 + 4 nch */
-        in.tail = tail || __ballot((uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4);
+        /* x4 loads reach pb + 4 nch: word loads if that could pass the end of the reads */
+        in.tail = tail || __ballot(solo ? (uint64_t)oa + 4u * nch > (uint64_t)(nrm ? end_n : end_t)
+                                        : (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4);
         uint32_t v[LN_R];
         const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
         /* a read of minq >= 64 needs 16-bit records: the site goes to the group kernel */
