@@ -20,6 +20,6 @@ for cfg in "c2 30 30 67108864 cpu" "c3 100 60 33554432 cpu" "c5 500 500 1048576 
   timeout -k 10 500 python3 "$R/bench.py" --workload shard $cpu --steps 10 --warmup 2 --lt "$lt" --ln "$ln" --sites "$n" \
       > "$O/bench_$name.json" 2> "$O/bench_$name.err"
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_$name" -o run -- \
-      python3 "$R/bench.py" --workload shard --no-cpu --no-pmc --steps 5 --warmup 2 --lt "$lt" --ln "$ln" --sites "$n" > "$O/kt_$name.log" 2>&1)
+      python3 "$R/bench.py" --workload shard --no-cpu --no-pmc --no-host-fed --steps 5 --warmup 2 --lt "$lt" --ln "$ln" --sites "$n" > "$O/kt_$name.log" 2>&1)
   echo "$name $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('%.3e' % d['value'], d['roofline']['frac'])" "$O/bench_$name.json")"
 done

@@ -15,5 +15,5 @@ cat "$O/bench.json"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- \
-    python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu --no-pmc --strong-steps 0 "$@" > "$O/kt.log" 2>&1
+    python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu --no-pmc --no-host-fed --strong-steps 0 "$@" > "$O/kt.log" 2>&1
 echo done
