@@ -1653,22 +1653,26 @@ void ss_score_main(ss_score_args a)
  * sample, sorted by lane groups (round 3; replaces the wave-per-site network
  * of round 2's ss_score_wide).
  *
- * A sort unit is one (site, sample) of n reads; it takes U = 1, 2, 4, 8 or 16
- * lanes (128 reads each).  Every lane builds and sorts its 128 keys exactly as
- * the main kernel does (ln_keys, ln_levels: complemented high halves, packed
- * min / max), then the unit's lanes merge across lanes, level 256 .. 128 U of
- * the same flip-form bitonic network: a mirror stage with the partner lane
- * lane ^ (M - 1), cleaners with lane ^ M/4 .. lane ^ 1 (DPP within a row of
- * 16 lanes), the in-lane stage at distance 64 and the in-lane cleaners.  In a
+ * A sort unit is one (site, sample) of n reads; it takes U = ceil(n / 128)
+ * lanes (1 .. 16, 128 reads each; round 5) and sorts as a network of P = the
+ * power of two >= U lanes whose lanes U .. P - 1 are virtual (pads only).  A
+ * unit's reads are dealt to its lanes in 4-read chunks, round-robin, so one
+ * load instruction reads each unit's next 16 U contiguous bytes.  Every lane
+ * builds and sorts its keys exactly as the main kernel does (ln_keys,
+ * ln_levels: complemented high halves, packed min / max), then the unit's
+ * lanes merge across lanes, level 256 .. 128 P of the same flip-form bitonic
+ * network: a mirror stage with the unit's lane j ^ (M - 1), cleaners with
+ * j ^ M/4 .. j ^ 1 (ds_bpermute from the unit's first lane: no alignment
+ * needed), the in-lane stage at distance 64 and the in-lane cleaners.  In a
  * cross-lane stage the lower lane keeps the minimum elements: in this layout
  * that is min in the low half and max in the (complemented) high half, one
- * v_bfi_b32 per register with a per-lane mask.  Units are laid out by
- * descending U, so every unit sits in one wave-sized batch of lanes and its
- * lanes are aligned; a batch merges up to its largest U (lanes of smaller
- * units sit the larger levels out).  The sorted contributing keys leave as
- * 8-bit fold records in the wave's record buffer (HBM / L2), per unit in
- * ascending order, and finish_sub does the 32-site fold, likelihoods and
- * decision.
+ * v_bfi_b32 per register with a per-lane mask; a lane whose partner is
+ * virtual keeps its registers (gp_xstage).  Units are packed by descending U,
+ * next-fit, so every unit sits in one wave-sized batch of lanes; a batch
+ * merges up to its largest P (lanes of smaller units sit the larger levels
+ * out).  The sorted contributing keys leave as 8-bit fold records in the
+ * wave's record buffer (HBM / L2), per unit in ascending order, and
+ * finish_sub does the 32-site fold, likelihoods and decision.
  * ------------------------------------------------------------------------ */
 namespace {
 
