@@ -16,6 +16,8 @@ Phases (round 3's SS_AB_* switches):
   nofin     no likelihoods / glf2cns (fields from the fold sums)
   nodecide  no site decision (score = tumor cns word)
   nominor   only the largest base group's chain per sample (the other three skipped)
+            (the kernel's own round-5 early exit is left in: it runs only without glf and
+            only in shallow batches, so a 60x/30x timing run never takes it)
   noload    reads synthesised in registers instead of loaded (key build without memory)
 and of ss_score_group (the C5 path):
   gnosort   no in-lane network (ln_levels)
@@ -31,17 +33,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "somatic-sniper_amd", "csrc", "ss_kernels.hip")
 
 EDITS = {
-    "nonet": [("            ln_levels<LN_R, 2>(v);\n            ln_records(", "            ln_records(")],
-    "norec": [("            ln_records(v, 4u * nch, L, lane);\n", "")],
-    "nofold": [("                ln_fold(L, lane, k ? tot_a : 0u, k ? acc.cnt_b : acc.cnt_a, fk, es, fs, c);\n",
-                "                for (int b = 0; b < 4; ++b) { es[b] = fs[b] = (float)(acc.cnt_a >> b); "
+    "nonet": [("        ln_levels<LN_R, 2>(v);\n        ln_records(", "        ln_records(")],
+    "norec": [("        ln_records(v, 4u * nch, L, lane);\n", "")],
+    "nofold": [("            ln_fold(L, lane, k ? tot_a : 0u, k ? acc.cnt_b : acc.cnt_a, fk, es, fs, c);\n",
+                "            for (int b = 0; b < 4; ++b) { es[b] = fs[b] = (float)(acc.cnt_a >> b); "
                 "c[b] = (acc.cnt_a >> (8 * b)) & 0xffu; }\n")],
-    "nofin": [("                ln_finish(es, fs, c, smpN ? nn : nt, k ? acc.rms_b : acc.rms_a, a.m, l03, l47, l89, cn, mq);\n",
-               "                l03 = __float_as_uint(es[0]); l47 = __float_as_uint(fs[1]); l89 = c[2]; "
+    "nofin": [("            ln_finish(es, fs, c, smpN ? nn : nt, k ? acc.rms_b : acc.rms_a, a.m, l03, l47, l89, cn, mq);\n",
+               "            l03 = __float_as_uint(es[0]); l47 = __float_as_uint(fs[1]); l89 = c[2]; "
                "cn = 0x11000000u; mq = c[3];\n")],
-    "nodecide": [("        if (ok) decide_site(kernarg_args(), qtab, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);\n",
-                  "        if (ok) a.score[s] = (int)L.res[lane][0].cns;\n")],
-    "nominor": [("        ln_chain(L, lane, st[b], isbig ? 0u : c[b], fk, eb, fb);\n",
+    "nodecide": [("    if (ok) decide_site(kernarg_args(), qtab, s, refc | ref16 << 8, L.res[lane][0], L.res[lane][1]);\n",
+                  "    if (ok) a.score[s] = (int)L.res[lane][0].cns;\n")],
+    "nominor": [("    if (!__ballot(max(max(no[0], no[1]), no[2]) > 6u)) {\n",
+                 "    if (true) {\n        es[0] = es[1] = es[2] = es[3] = e; fs[0] = fs[1] = fs[2] = fs[3] = f;\n        return;\n"),
+                ("        ln_chain(L, lane, st[b], isbig ? 0u : c[b], fk, eb, fb);\n",
                  "        eb = fb = 0.0f;\n")],
     "noload": [("    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */\n",
                 "    if (true) {\n#pragma unroll\n        for (int t = 0; t < 4; ++t) "
