@@ -1426,27 +1426,8 @@ __device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, boo
     wave_sync();
 }
 
-/* Early exit of the lane path (round 5, DESIGN.md 4.1), for shallow blocks:
- * before any key is built, a count pass over a site's reads decides the sites
- * whose result needs no likelihood at all and writes their score; the others
- * are queued for ln_block.  Exact -- the reference's own outcome -- and never
- * taken when glf records are requested:
- *   - ref char 'N' or an empty sample: -1 (somatic_sniper.c:127);
- *   - a reference code of 15 other than 'N' ('n', ...): 255, never an SNV
- *     candidate (:156);
- *   - reference A/C/G/T, every read of both samples on the reference base
- *     (bam_nt16_nt4_table semantics, sniper_maqcns.c:153-154: N/IUPAC reads
- *     count as A, '=' as the reference) and enough reads of minq >= 24: 255.
- *     Then in each sample the reference homozygote has p = 0 (tmp2 = 0,
- *     :196) and every other homozygote p = esum + coef[bar_e][n][n] with
- *     esum >= 24 * (fk[0] + .. + fk[c24 - 1]) (the walk visits the c24 reads
- *     of q >= 24 first, each with a weight fk[w] >= fk[k]); the host table
- *     SS_TAB_FAST holds, per read count n, the smallest c24 that makes that
- *     >= 1 for every bar_e and every n' <= n (ss_capi.hip fast_table), so
- *     those homozygotes quantise to lk >= 1, the heterozygotes score
- *     >= q_r >= 1 (SS_MF_FAST requires it), and sniper_glf2cns (:250-273)
- *     calls the reference homozygote in both samples: no candidate.
- * Returns true when it wrote the site's score. */
+/* the early exit's count pass over chunk c (ln_classify): per-sample group
+ * counts of every read (contributing or not) and the reads of minq >= 24 */
 __device__ __forceinline__ void ln_count_chunk(const LaneIn &in, const uint2 *lut, uint32_t c, const uint32_t (&x)[4],
                                                uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24)
 {
@@ -1475,6 +1456,27 @@ __device__ __forceinline__ void ln_count_chunk(const LaneIn &in, const uint2 *lu
     c24 += fa ? q : q << 16;
 }
 
+/* Early exit of the lane path (round 5, DESIGN.md 4.1), for shallow blocks:
+ * before any key is built, a count pass over a site's reads decides the sites
+ * whose result needs no likelihood at all and writes their score; the others
+ * are queued for ln_block.  Exact -- the reference's own outcome -- and never
+ * taken when glf records are requested:
+ *   - ref char 'N' or an empty sample: -1 (somatic_sniper.c:127);
+ *   - a reference code of 15 other than 'N' ('n', ...): 255, never an SNV
+ *     candidate (:156);
+ *   - reference A/C/G/T, every read of both samples on the reference base
+ *     (bam_nt16_nt4_table semantics, sniper_maqcns.c:153-154: N/IUPAC reads
+ *     count as A, '=' as the reference) and enough reads of minq >= 24: 255.
+ *     Then in each sample the reference homozygote has p = 0 (tmp2 = 0,
+ *     :196) and every other homozygote p = esum + coef[bar_e][n][n] with
+ *     esum >= 24 * (fk[0] + .. + fk[c24 - 1]) (the walk visits the c24 reads
+ *     of q >= 24 first, each with a weight fk[w] >= fk[k]); the host table
+ *     SS_TAB_FAST holds, per read count n, the smallest c24 that makes that
+ *     >= 1 for every bar_e and every n' <= n (ss_capi.hip fast_table), so
+ *     those homozygotes quantise to lk >= 1, the heterozygotes score
+ *     >= q_r >= 1 (SS_MF_FAST requires it), and sniper_glf2cns (:250-273)
+ *     calls the reference homozygote in both samples: no candidate.
+ * Returns true when it wrote the site's score. */
 __device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 *lut, uint32_t s, bool insite,
                                             uint32_t end_t, uint32_t end_n)
 {
