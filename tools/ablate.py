@@ -19,12 +19,16 @@ Phases (round 3's SS_AB_* switches):
             (the kernel's own round-5 early exit is left in: it runs only without glf and
             only in shallow batches, so a 60x/30x timing run never takes it)
   noload    reads synthesised in registers instead of loaded (key build without memory)
+  fdep      the long chains' float accumulations split in two interleaved chains (odd / even
+            records, summed at the end of each 4-record step): half the serial f64 depth,
+            the same instructions plus two adds -- how much the fold waits on its own latency
 and of ss_score_group (the C5 path):
   gnosort   no in-lane network (ln_levels)
   gnomerge  no cross-lane merge levels (gp_level)
   gnorec    no fold records written to the arena
   gnofold   no ordered fold in finish_sub (sums from the counts)
   gnofin    no likelihoods in finish_sub (p from the sums)
+  gfdep     fdep for finish_sub's chains
 """
 import os
 import sys
@@ -51,6 +55,26 @@ EDITS = {
                 "    if (true) {\n#pragma unroll\n        for (int t = 0; t < 4; ++t) "
                 "x[t] = ((in.na + 4u * c + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;\n        return;\n    }\n"
                 "    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */\n")],
+    "fdep": [("        if (TAIL) w8 = (uint32_t)j < m ? w8 : 8u * LN_FK_ZERO;\n        W += 8u << sh;\n"
+              "        t[j] = *reinterpret_cast<const double *>(fkb + w8);\n    }\n"
+              "#pragma unroll\n    for (int j = 0; j < 4; ++j) {\n        const uint32_t q = (R >> (24 - 8 * j)) & 63u;\n"
+              "        e = (float)((double)e + t[j] * (double)q);\n        f = (float)((double)f + t[j]);\n    }\n",
+              "        if (TAIL) w8 = (uint32_t)j < m ? w8 : 8u * LN_FK_ZERO;\n        W += 8u << sh;\n"
+              "        t[j] = *reinterpret_cast<const double *>(fkb + w8);\n    }\n"
+              "    float e2 = 0.0f, f2 = 0.0f;\n#pragma unroll\n    for (int j = 0; j < 4; ++j) {\n"
+              "        const uint32_t q = (R >> (24 - 8 * j)) & 63u;\n        if (j & 1) { e2 = (float)((double)e2 + t[j] * (double)q); "
+              "f2 = (float)((double)f2 + t[j]); }\n        else { e = (float)((double)e + t[j] * (double)q); "
+              "f = (float)((double)f + t[j]); }\n    }\n    e += e2;\n    f += f2;\n")],
+    "gfdep": [("        if (TAIL) w8 = j < m ? w8 : 8u * GP_FK_ZERO;\n        W += 8u << sh;\n"
+               "        t[j] = *reinterpret_cast<const double *>(fkb + w8);\n    }\n"
+               "#pragma unroll\n    for (int j = 0; j < 4; ++j) {\n        const uint32_t q = (R >> (24 - 8 * j)) & 63u;\n"
+               "        e = (float)((double)e + t[j] * (double)q);\n        f = (float)((double)f + t[j]);\n    }\n",
+               "        if (TAIL) w8 = j < m ? w8 : 8u * GP_FK_ZERO;\n        W += 8u << sh;\n"
+               "        t[j] = *reinterpret_cast<const double *>(fkb + w8);\n    }\n"
+               "    float e2 = 0.0f, f2 = 0.0f;\n#pragma unroll\n    for (int j = 0; j < 4; ++j) {\n"
+               "        const uint32_t q = (R >> (24 - 8 * j)) & 63u;\n        if (j & 1) { e2 = (float)((double)e2 + t[j] * (double)q); "
+               "f2 = (float)((double)f2 + t[j]); }\n        else { e = (float)((double)e + t[j] * (double)q); "
+               "f = (float)((double)f + t[j]); }\n    }\n    e += e2;\n    f += f2;\n")],
     "gnosort": [("            ln_levels<LN_R, 2>(v);\n            if (__ballot(act && uP >= 2u))",
                  "            if (__ballot(act && uP >= 2u))")],
     "gnomerge": [("            if (__ballot(act && uP >= 2u)) { if (act && uP >= 2u) gp_level<2>(v, j, pb, uU); }\n"
