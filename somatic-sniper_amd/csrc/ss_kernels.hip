@@ -1118,11 +1118,16 @@ __device__ __forceinline__ void ln_records(uint32_t (&v)[LN_R], uint32_t nel, La
  * end a read takes fk's zero entry (LN_FK_ZERO), which leaves e and f as they
  * are (x + 0.0 == x), so lanes of shorter chains need no mask. */
 #define LN_FK_ZERO 256
+/* fk entries the lane path can use: a chain holds at most LN_N = 128 records,
+ * so w <= 127; the main kernel's LDS copy keeps entries 128 .. 256 zero, and a
+ * lane that sits a step out reads from there (ln_chain) */
+#define LN_FK_LIVE 128
 
 /* four steps of a chain from the window R of records k0 - 3 .. k0; steps
  * j >= m (past the chain's end) read fk's zero entry */
 template <bool TAIL>
-__device__ __forceinline__ void ln_steps(const char *fkb, uint32_t R, uint32_t m, uint32_t &W, float &e, float &f)
+__device__ __forceinline__ void ln_steps(const char *fkb, uint32_t R, uint32_t m, uint32_t inc, uint32_t &W, float &e,
+                                         float &f)
 {
     double t[4];
 #pragma unroll
@@ -1131,7 +1136,7 @@ __device__ __forceinline__ void ln_steps(const char *fkb, uint32_t R, uint32_t m
         const uint32_t sh = (r >> 2) & 16u;                       /* strand << 4 */
         uint32_t w8 = __builtin_amdgcn_ubfe(W, sh, 16u);
         if (TAIL) w8 = (uint32_t)j < m ? w8 : 8u * LN_FK_ZERO;
-        W += 8u << sh;
+        W += inc << sh;
         t[j] = *reinterpret_cast<const double *>(fkb + w8);
     }
 #pragma unroll
@@ -1158,22 +1163,25 @@ __device__ __forceinline__ void ln_chain(const LaneLds &L, uint32_t lane, uint32
     f = 0.0f;
     uint32_t W = 0;                  /* strand 0 count in bits 0..15, strand 1 in 16..31 (units of 8 B) */
     /* whole groups of four steps; a lane whose chain has fewer left computes
-     * them on a harmless window and keeps its old state (selects, not an exec
-     * mask: the masked form cost phi copies and exec bookkeeping every step,
-     * 4.5% of the kernel) */
-    for (uint32_t i = 0; __ballot(i + 4u <= n); i += 4u) {
-        const bool act = i + 4u <= n;
-        float e2 = e, f2 = f;
-        uint32_t W2 = W;
-        ln_steps<false>(fkb, ln_window(colw, act ? s0 + n - i : 3u), 4u, W2, e2, f2);
-        e = act ? e2 : e;
-        f = act ? f2 : f;
-        W = act ? W2 : W;
+     * them on a harmless window without counting, its counters moved into
+     * fk's zeroed upper half (w <= 127: entries 128 .. 255), so e and f stay
+     * as they are (no exec mask: the masked form cost phi copies and exec
+     * bookkeeping every step, 4.5% of the kernel) */
+    const uint32_t zw = 8u * LN_FK_LIVE * 0x10001u;
+    if (__ballot(n >= 4u)) {
+        uint32_t i = 0;
+        do {
+            const bool act = i + 4u <= n;
+            W = act ? W : W | zw;
+            ln_steps<false>(fkb, ln_window(colw, act ? s0 + n - i : 3u), 4u, act ? 8u : 0u, W, e, f);
+            i += 4u;
+        } while (__ballot(i + 4u <= n));
+        W &= ~zw;
     }
     /* the lane's last 1..3 steps */
     const uint32_t i = n & ~3u;
     if (__ballot(i < n))
-        if (i < n) ln_steps<true>(fkb, ln_window(colw, s0 + n - i), n - i, W, e, f);
+        if (i < n) ln_steps<true>(fkb, ln_window(colw, s0 + n - i), n - i, 8u, W, e, f);
 }
 
 /* the three groups other than the lane's largest, walked together: one record
@@ -1190,7 +1198,9 @@ __device__ __forceinline__ void ln_chain3(const LaneLds &L, uint32_t lane, const
     const uint32_t mx = max(max(n[0], n[1]), n[2]);
 #pragma unroll
     for (int k = 0; k < 3; ++k) { e[k] = 0.0f; f[k] = 0.0f; }
-    for (uint32_t i = 0; __ballot(i < mx); ++i) {
+    if (!__ballot(mx > 0u)) return;
+    uint32_t i = 0;
+    do {
         uint32_t r[3];
         double t[3];
 #pragma unroll
@@ -1208,7 +1218,8 @@ __device__ __forceinline__ void ln_chain3(const LaneLds &L, uint32_t lane, const
             e[k] = (float)((double)e[k] + t[k] * (double)(r[k] & 63u));
             f[k] = (float)((double)f[k] + t[k]);
         }
-    }
+        ++i;
+    } while (__ballot(i < mx));
 }
 
 /* fold of one sample: group sizes cnt (8-bit fields), records from s0 */
@@ -1562,7 +1573,7 @@ void ss_score_main(ss_score_args a)
      * in [-512, 0]; 2 KB keeps 3 workgroups per CU within 160 KB) */
     __shared__ int16_t qtab[1024];
     __shared__ uint16_t qq[LN_WAVES][128];          /* the early exit's queue: 63 carried + 64 new sites */
-    for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < 256u ? ss_tab_fk(a.m)[i] : 0.0;
+    for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < LN_FK_LIVE ? ss_tab_fk(a.m)[i] : 0.0;
     for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) qtab[i] = (int16_t)ss_tab_qadd(a.m)[i];
     ln_lut_build(lut);
     __syncthreads();
