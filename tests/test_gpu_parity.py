@@ -383,6 +383,29 @@ def test_quirk_parity(pkg, oracle, opts):
     assert score[12] == 255                       # ref n: scored, not a candidate
 
 
+@pytest.mark.parametrize("opts", [[], ["-J"]])
+def test_single_strand_chains_parity(pkg, oracle, opts):
+    """Fold chains as long as the lane path allows on one strand: w runs up to
+    127, the last fk entry the main kernel's LDS copy keeps (entries 128 .. 255
+    are zeros that lanes with fewer than four records left read, ln_chain).
+    128 + 128 reads (separate mode), 100 + 28 (joint mode), 128 reads of a
+    non-reference base, and a block of such sites next to shallow ones so that
+    most lanes sit the long steps out."""
+    R = lambda mq, bq, nt, st=0: _r(pkg, mq, bq, nt, st)
+    A, C_, G, T = 1, 2, 4, 8
+    s = []
+    for k in range(3):
+        s.append(("A", [R(60, 10 + (i * 7 + k) % 31, T, 0) for i in range(128)],
+                  [R(60, 20 + (i * 3 + k) % 17, T, 1) for i in range(128)]))
+        s.append(("G", [R(60, 5 + (i * 11 + k) % 40, G, 1) for i in range(100)],
+                  [R(60, 30, G, 0)] * 27 + [R(60, 30, A, 0)]))
+        s.append(("C", [R(60, 4 + (i * 5 + k) % 50, A, k & 1) for i in range(128)],
+                  [R(60, 33, C_, 0)] * 40))
+    for i in range(64 - len(s)):
+        s.append(("T", [R(60, 30, T, i & 1)] * (1 + i % 5), [R(60, 30, T, 0)] * (1 + i % 3)))
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(s), opts)
+
+
 def all_reference_sites(pkg):
     """Sites whose every read is on the reference base (round 5 measured an
     early exit for them): the count of reads of minq >= 24
