@@ -1122,6 +1122,8 @@ __device__ __forceinline__ void ln_records(uint32_t (&v)[LN_R], uint32_t nel, La
  * so w <= 127; the main kernel's LDS copy keeps entries 128 .. 256 zero, and a
  * lane that sits a step out reads from there (ln_chain) */
 #define LN_FK_LIVE 128
+static_assert(LN_FK_LIVE >= LN_N && 2 * LN_FK_LIVE <= LN_FK_ZERO,
+              "a lane's counters (w < LN_N) must stay below the zeroed half, and w + LN_FK_LIVE inside the table");
 
 /* four steps of a chain from the window R of records k0 - 3 .. k0; steps
  * j >= m (past the chain's end) read fk's zero entry */
