@@ -55,11 +55,11 @@ EDITS = {
                 "    if (true) {\n#pragma unroll\n        for (int t = 0; t < 4; ++t) "
                 "x[t] = ((in.na + 4u * c + (uint32_t)t) * 0x9E3779B1u) & 0x001f3f3fu;\n        return;\n    }\n"
                 "    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */\n")],
-    "fdep": [("        if (TAIL) w8 = (uint32_t)j < m ? w8 : 8u * LN_FK_ZERO;\n        W += 8u << sh;\n"
+    "fdep": [("        if (TAIL) w8 = (uint32_t)j < m ? w8 : 8u * LN_FK_ZERO;\n        W += inc << sh;\n"
               "        t[j] = *reinterpret_cast<const double *>(fkb + w8);\n    }\n"
               "#pragma unroll\n    for (int j = 0; j < 4; ++j) {\n        const uint32_t q = (R >> (24 - 8 * j)) & 63u;\n"
               "        e = (float)((double)e + t[j] * (double)q);\n        f = (float)((double)f + t[j]);\n    }\n",
-              "        if (TAIL) w8 = (uint32_t)j < m ? w8 : 8u * LN_FK_ZERO;\n        W += 8u << sh;\n"
+              "        if (TAIL) w8 = (uint32_t)j < m ? w8 : 8u * LN_FK_ZERO;\n        W += inc << sh;\n"
               "        t[j] = *reinterpret_cast<const double *>(fkb + w8);\n    }\n"
               "    float e2 = 0.0f, f2 = 0.0f;\n#pragma unroll\n    for (int j = 0; j < 4; ++j) {\n"
               "        const uint32_t q = (R >> (24 - 8 * j)) & 63u;\n        if (j & 1) { e2 = (float)((double)e2 + t[j] * (double)q); "
