@@ -93,10 +93,13 @@ __device__ __forceinline__ int bar_e_fast(float e, float f)
 {
     const float r = e * __builtin_amdgcn_rcpf(f) + 0.5f;
     const float fr = __builtin_amdgcn_fractf(r);
-    const bool near = fr < 0x1p-12f || fr > 1.0f - 0x1p-12f;
+    /* near an integer (fr < 2^-12 or > 1 - 2^-12) as one compare whose lane
+     * mask is the ballot itself (a ballot of an OR of two compares went
+     * through a VGPR and back); at the band's edges either path is exact */
+    const float d = __builtin_fabsf(fr - 0.5f);
     int be = (int)__builtin_floorf(r);
-    if (__ballot(near)) {
-        if (near) be = (int)((double)(e / f) + 0.5);
+    if (__ballot(d > 0.5f - 0x1p-12f)) {
+        if (d > 0.5f - 0x1p-12f) be = (int)((double)(e / f) + 0.5);
     }
     be = be < 4 ? 4 : be;
     return be > 63 ? 63 : be;
@@ -201,7 +204,10 @@ __device__ __forceinline__ void geno_p_range(uint32_t role, const float es[4], c
         }
         const bool hom = j == k;
         const uint32_t il = hom ? 0u : (c[j] << 8 | c[k]);
-        const uint32_t ic = c2 ? ((uint32_t)bar_e_fast(e, f) << 16 | tot << 8 | c2) : 0u;
+        /* bar_e for every lane (no branch on c2: f = 0 gives a NaN quotient,
+         * which is not near an integer, and the index is not used) */
+        const uint32_t be = (uint32_t)bar_e_fast(e, f);
+        const uint32_t ic = c2 ? (be << 16 | tot << 8 | c2) : 0u;
         lhv[t] = ss_tab_lhet(m)[il];
         cfv[t] = ss_tab_coef(m)[ic];
         ev[t] = e;
