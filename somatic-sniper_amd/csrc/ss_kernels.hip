@@ -943,8 +943,15 @@ struct LaneIn {
     uint32_t la, lb;                 /* A's and B's lookup rows (ln_lut_row) */
     uint32_t clast;                  /* CLAMP loads: chunks past this one load it again */
     uint32_t cstep;                  /* STRIDE: words from one chunk of the lane to its next */
-    bool tail;                       /* wave-uniform: an x4 load could pass the end of the reads */
+    uint32_t tail;                   /* wave-uniform (an SGPR, 0 / 1): an x4 load could pass the end of the reads */
 };
+
+/* a wave-uniform flag as an SGPR integer: branches on it stay scalar (a bool
+ * kept across the chunk loads was re-materialised in a VGPR at every load) */
+__device__ __forceinline__ uint32_t ln_uniform(bool b)
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane(b ? 1 : 0);
+}
 
 struct LaneAcc {
     uint32_t rms_a, rms_b, cnt_a, cnt_b;
@@ -958,13 +965,14 @@ struct LaneAcc {
  * is the instruction's immediate and the loads in flight stay in fixed
  * registers.  In a tail block (the batch's last sites, or a batch of fewer
  * than 4 reads) the lane loads word by word, only its own reads. */
-template <bool CLAMP, bool STRIDE>
+/* TM: 0 = test in.tail at every load, 1 = the caller knows it is 0, 2 = 1 */
+template <bool CLAMP, bool STRIDE, int TM = 0>
 __device__ __forceinline__ void ln_load(const LaneIn &in, uint32_t c, uint32_t (&x)[4])
 {
     const bool fa = c < in.nca;
     const uint32_t cc = CLAMP ? min(c, in.clast) : c;
     const uint32_t *src = (fa ? in.pa : in.pb) + (STRIDE ? cc * in.cstep : 4u * cc);
-    if (in.tail) {                   /* wave-uniform: word loads, none past the lane's reads */
+    if (TM == 2 || (TM == 0 && in.tail)) {   /* wave-uniform: word loads, none past the lane's reads */
         const int lim = (int)(fa ? in.na : in.nab) - (int)(STRIDE ? c * in.cstep : 4u * c);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -1041,7 +1049,7 @@ __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint2 *lut, uin
     acc.cnt_a += fa ? ccnt : 0u;
 }
 
-template <bool CLAMP = false, bool STRIDE = false>
+template <bool CLAMP = false, bool STRIDE = false, int TM = 0>
 __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint2 *lut, uint32_t nch, uint32_t cap,
                                            uint32_t (&v)[LN_R])
 {
@@ -1055,14 +1063,14 @@ __device__ __forceinline__ LaneAcc ln_keys(const LaneIn &in, const uint2 *lut, u
     uint32_t buf[2][LN_P][4];
     if (nch > 0u) {
 #pragma unroll
-        for (int j = 0; j < LN_P; ++j) ln_load<CLAMP, STRIDE>(in, (uint32_t)j, buf[0][j]);
+        for (int j = 0; j < LN_P; ++j) ln_load<CLAMP, STRIDE, TM>(in, (uint32_t)j, buf[0][j]);
     }
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
         if ((uint32_t)(g * LN_P) >= nch) continue;
         if (g + 1 < NG && (uint32_t)((g + 1) * LN_P) < nch) {
 #pragma unroll
-            for (int j = 0; j < LN_P; ++j) ln_load<CLAMP, STRIDE>(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
+            for (int j = 0; j < LN_P; ++j) ln_load<CLAMP, STRIDE, TM>(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
         }
 #pragma unroll
         for (int j = 0; j < LN_P; ++j) ln_chunk<STRIDE>(in, lut, (uint32_t)(g * LN_P + j), cap, buf[g & 1][j], v, acc);
@@ -1384,10 +1392,14 @@ __device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, boo
         in.lb = ln_lut_row(17u + ref16);
         const uint32_t nch = wave_max((in.nab + 3u) >> 2);
         /* x4 loads reach pb + 4 nch: word loads if that could pass the end of the reads */
-        in.tail = tail || __ballot(solo ? (uint64_t)oa + 4u * nch > (uint64_t)(nrm ? end_n : end_t)
-                                        : (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4);
+        in.tail = ln_uniform(tail || __ballot(solo ? (uint64_t)oa + 4u * nch > (uint64_t)(nrm ? end_n : end_t)
+                                                   : (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4));
         uint32_t v[LN_R];
-        const LaneAcc acc = ln_keys(in, lut, nch, cap, v);
+        /* the tail test once per pass, not at every chunk load (the common
+         * case has no word-load path at all) */
+        LaneAcc acc;
+        if (in.tail) acc = ln_keys<false, false, 2>(in, lut, nch, cap, v);
+        else acc = ln_keys<false, false, 1>(in, lut, nch, cap, v);
         /* a read of minq >= 64 needs 16-bit records: the site goes to the group kernel */
         wild = wild || acc.maxq >= 64u;
         ln_levels<LN_R, 2>(v);
@@ -1535,9 +1547,9 @@ __device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 
         in.lb = ln_lut_row(17u + ref16);
         const uint32_t nch = wave_max((in.nab + 3u) >> 2);
         /* as in ln_block: word loads when an x4 load could pass the end of the reads */
-        in.tail = __ballot((uint64_t)oa + in.na4 > (uint64_t)end_t ||
-                           (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4) ||
-                  end_t < 4u || end_n < 4u;
+        in.tail = ln_uniform(__ballot((uint64_t)oa + in.na4 > (uint64_t)end_t ||
+                                      (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4) ||
+                             end_t < 4u || end_n < 4u);
         uint32_t cnt_a = 0, cnt_t = 0, c24 = 0;
         /* groups of LN_P chunk loads in flight, as in ln_keys */
         uint32_t buf[2][LN_P][4];
@@ -1930,7 +1942,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
             in.pb = in.pa;
             in.la = in.lb = ln_lut_row(1u + smp * 16u + ((L.c_ref[wv][site_l] >> 8) & 0xffu));
             const uint32_t endv = smp ? end_n : end_t;
-            in.tail = __ballot((uint64_t)start + last_w > (uint64_t)endv) || end_t < 4u || end_n < 4u;
+            in.tail = ln_uniform(__ballot((uint64_t)start + last_w > (uint64_t)endv) || end_t < 4u || end_n < 4u);
             uint32_t v[LN_R];
             const LaneAcc acc = ln_keys<true, true>(in, lut, nch, cap, v);
             /* the unit's counts before the sort: acc is not live across it */
