@@ -1487,6 +1487,29 @@ __device__ __forceinline__ void ln_count_chunk(const LaneIn &in, const uint2 *lu
     c24 += fa ? q : q << 16;
 }
 
+/* the count pass over a block's chunks: groups of LN_P chunk loads in flight,
+ * as in ln_keys, the tail mode fixed per instantiation (TM, ln_load) */
+template <int TM>
+__device__ __forceinline__ void ln_count_pass(const LaneIn &in, const uint2 *lut, uint32_t nch, uint32_t &cnt_a,
+                                              uint32_t &cnt_t, uint32_t &c24)
+{
+    uint32_t buf[2][LN_P][4];
+    if (nch > 0u) {
+#pragma unroll
+        for (int j = 0; j < LN_P; ++j) ln_load<false, false, TM>(in, (uint32_t)j, buf[0][j]);
+    }
+#pragma unroll
+    for (int g = 0; g < LN_C / LN_P; ++g) {
+        if ((uint32_t)(g * LN_P) >= nch) break;
+        if (g + 1 < LN_C / LN_P && (uint32_t)((g + 1) * LN_P) < nch) {
+#pragma unroll
+            for (int j = 0; j < LN_P; ++j) ln_load<false, false, TM>(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
+        }
+#pragma unroll
+        for (int j = 0; j < LN_P; ++j) ln_count_chunk(in, lut, (uint32_t)(g * LN_P + j), buf[g & 1][j], cnt_a, cnt_t, c24);
+    }
+}
+
 /* Early exit of the lane path (round 5), for shallow blocks:
  * before any key is built, a count pass over a site's reads decides the sites
  * whose result needs no likelihood at all and writes their score; the others
@@ -1551,22 +1574,8 @@ __device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 
                                       (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4) ||
                              end_t < 4u || end_n < 4u);
         uint32_t cnt_a = 0, cnt_t = 0, c24 = 0;
-        /* groups of LN_P chunk loads in flight, as in ln_keys */
-        uint32_t buf[2][LN_P][4];
-        if (nch > 0u) {
-#pragma unroll
-            for (int j = 0; j < LN_P; ++j) ln_load<false, false>(in, (uint32_t)j, buf[0][j]);
-        }
-#pragma unroll
-        for (int g = 0; g < LN_C / LN_P; ++g) {
-            if ((uint32_t)(g * LN_P) >= nch) break;
-            if (g + 1 < LN_C / LN_P && (uint32_t)((g + 1) * LN_P) < nch) {
-#pragma unroll
-                for (int j = 0; j < LN_P; ++j) ln_load<false, false>(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
-            }
-#pragma unroll
-            for (int j = 0; j < LN_P; ++j) ln_count_chunk(in, lut, (uint32_t)(g * LN_P + j), buf[g & 1][j], cnt_a, cnt_t, c24);
-        }
+        if (in.tail) ln_count_pass<2>(in, lut, nch, cnt_a, cnt_t, c24);
+        else ln_count_pass<1>(in, lut, nch, cnt_a, cnt_t, c24);
         const uint32_t sh = 8u * (uint32_t)__builtin_ctz(ref16 | 16u);   /* the reference base's count field */
         const uint32_t cnt_b = cnt_t - cnt_a;
         const uint32_t tot_a = (cnt_a & 0xffu) + (cnt_a >> 8 & 0xffu) + (cnt_a >> 16 & 0xffu) + (cnt_a >> 24);
@@ -1944,7 +1953,9 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
             const uint32_t endv = smp ? end_n : end_t;
             in.tail = ln_uniform(__ballot((uint64_t)start + last_w > (uint64_t)endv) || end_t < 4u || end_n < 4u);
             uint32_t v[LN_R];
-            const LaneAcc acc = ln_keys<true, true>(in, lut, nch, cap, v);
+            LaneAcc acc;
+            if (in.tail) acc = ln_keys<true, true, 2>(in, lut, nch, cap, v);
+            else acc = ln_keys<true, true, 1>(in, lut, nch, cap, v);
             /* the unit's counts before the sort: acc is not live across it */
             if (act) {
                 const uint32_t c = acc.cnt_a;
