@@ -1953,9 +1953,7 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
             const uint32_t endv = smp ? end_n : end_t;
             in.tail = ln_uniform(__ballot((uint64_t)start + last_w > (uint64_t)endv) || end_t < 4u || end_n < 4u);
             uint32_t v[LN_R];
-            LaneAcc acc;
-            if (in.tail) acc = ln_keys<true, true, 2>(in, lut, nch, cap, v);
-            else acc = ln_keys<true, true, 1>(in, lut, nch, cap, v);
+            const LaneAcc acc = ln_keys<true, true>(in, lut, nch, cap, v);
             /* the unit's counts before the sort: acc is not live across it */
             if (act) {
                 const uint32_t c = acc.cnt_a;
