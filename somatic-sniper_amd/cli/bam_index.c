@@ -59,17 +59,23 @@ bad:
     return NULL;
 }
 
-/* an index whose mtime is an earlier second than its BAM's is stale: it may
- * describe a file since rewritten.  htslib makes the same whole-second test
- * (hts.c idx_test_and_fetch) but only warns and uses the index; here it is not
- * used and the CLI takes the streaming walk instead (same output, no
- * contig-parallel pileup).  An index written in the same second as its BAM is
- * used, as in htslib; bai_check_start still verifies it against the file. */
+/* an index older than its BAM is stale: it may describe a file since
+ * rewritten; it is not used and the CLI takes the streaming walk instead (same
+ * output, no contig-parallel pileup).  When both mtimes carry nanoseconds
+ * (tv_nsec != 0 on both) they are compared to the nanosecond, so an index
+ * written earlier in the same second as a rewrite of its BAM is refused.  On
+ * a second-resolution filesystem, or for copies that kept only seconds, the
+ * test is htslib's whole-second one (hts.c idx_test_and_fetch, which only
+ * warns): an index of the same second is used, and bai_check_start still
+ * verifies it against the file. */
 static bai_t *bai_load_fresh(const char *idx_path, const struct stat *bam_st)
 {
     struct stat st;
     if (stat(idx_path, &st) != 0) return NULL;
     if (st.st_mtime < bam_st->st_mtime) return NULL;
+    if (st.st_mtime == bam_st->st_mtime && st.st_mtim.tv_nsec != 0 && bam_st->st_mtim.tv_nsec != 0 &&
+        st.st_mtim.tv_nsec < bam_st->st_mtim.tv_nsec)
+        return NULL;
     return bai_load(idx_path);
 }
 

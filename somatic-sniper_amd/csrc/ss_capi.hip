@@ -121,8 +121,13 @@ extern "C" const char *ss_strerror(int code)
  *
  * Round 4 took device memory from the stream-ordered pool (hipMallocAsync /
  * hipFreeAsync); contexts created while other contexts of the process were
- * being destroyed then lost batches (tools/pool_race.hip
- * reproduces it without any kernel of ours).
+ * being destroyed then lost batches in the CLI's contig-group mode (4 of 25
+ * runs).  The cause is NOT established: a standalone
+ * stand-in without our kernels (tools/pool_race.hip) did not reproduce it in
+ * 160 contexts, and a host wait after every hipMallocAsync (0 of 40 bad) fits
+ * a cross-context release inside the runtime's pool and a stream-ordering gap
+ * on our side equally well.  This allocator avoids both: no pool, and no
+ * block is reused before the device is done with it.
  *
  * Debug build (make debug, -DSS_DEBUG_CANARY): every block carries guard bands
  * of SS_GUARD bytes before and after it, filled with 0xA5 at allocation and
@@ -271,19 +276,28 @@ static void ctx_quiesce(ss_ctx_t *c)
 
 /* The main kernel's early exit (ss_kernels.hip ln_classify): for n = 1 .. 128
  * reads per sample, the smallest count c24 of reads with minq >= 24 such that
- *   24 * (fk[0] + .. + fk[c24 - 1]) * (1 - 1e-4) + min coef[q][n'][n'] >= 1
+ *   24 * (m[0] + .. + m[c24 - 1]) * (1 - 1e-4) + min coef[q][n'][n'] >= 1,
+ *   m[k] = min(fk[0 .. k]),
  * over q in [4, 63] and n' in [1, n] (sniper_maqcns.c:184-196: the non-reference
- * homozygotes' p when every read is on the reference); 255 = never.  The
- * 1e-4 margin covers the float accumulation of esum (<= 128 roundings of
- * 2^-24 relative each).  Enabled only with q_r >= 1, so a heterozygote never
- * ties the reference homozygote in sniper_glf2cns. */
+ * homozygotes' p when every read is on the reference); 255 = never.  The k-th
+ * q >= 24 read of the walk weighs fk[w] with w <= k (w counts per strand), so
+ * its weight is >= m[k] whatever the shape of fk: fk[n] = theta^n (1 - eta) +
+ * eta (sniper_maqcns.c:72) decreases for theta < 1 but increases for the
+ * theta > 1 that -T accepts (main.c:83 has no range check), and then m[k] =
+ * fk[0].  The 1e-4 margin covers the float accumulation of esum (<= 128
+ * roundings of 2^-24 relative each).  Enabled only with q_r >= 1, so a
+ * heterozygote never ties the reference homozygote in sniper_glf2cns. */
 static int fast_table(const ss_host_model_t &hm, uint8_t thr[256])
 {
     memset(thr, 255, 256);
     if (hm.q_r_int < 1) return 0;
     double F[130];
     F[0] = 0.0;
-    for (int k = 0; k < 129; ++k) F[k + 1] = F[k] + hm.fk[k < 255 ? k : 255];
+    double run_min = hm.fk[0];
+    for (int k = 0; k < 129; ++k) {
+        run_min = std::min(run_min, hm.fk[k < 255 ? k : 255]);
+        F[k + 1] = F[k] + run_min;
+    }
     double cm = 1e300;
     int any = 0;
     for (int n = 1; n <= 128; ++n) {
@@ -298,23 +312,38 @@ static int fast_table(const ss_host_model_t &hm, uint8_t thr[256])
     return any;
 }
 
-/* fingerprint the context's device tables (ss_tab_fingerprint) and compare
- * with the host's sums; the caller's stream order puts this after the upload /
- * the launches it wants checked.  Synchronizes the context's stream. */
-static int tables_verify(ss_ctx_t *c)
+/* queue the fingerprint of the context's device tables (ss_tab_fingerprint)
+ * on the context's stream, after whatever it should check, and its copy to
+ * `dst` (3 words; page-locked, so the copy stays asynchronous) */
+static int tables_fp_enqueue(ss_ctx_t *c, unsigned long long *dst)
 {
-    unsigned long long fp[3] = {0, 0, 0};
     hipStream_t hs = c->hstream;
     unsigned long long *dfp = reinterpret_cast<unsigned long long *>(c->d_counters + 16);
-    HIPCHK(hipMemsetAsync(dfp, 0, sizeof fp, hs));
+    HIPCHK(hipMemsetAsync(dfp, 0, 3 * sizeof(unsigned long long), hs));
     if (ss_launch_tab_fingerprint(c->d_tab, dfp, hs) != 0) return SS_E_HIP;
-    HIPCHK(hipMemcpyAsync(fp, dfp, sizeof fp, hipMemcpyDeviceToHost, hs));
-    HIPCHK(hipStreamSynchronize(hs));
+    HIPCHK(hipMemcpyAsync(dst, dfp, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, hs));
+    return SS_OK;
+}
+
+/* compare a completed fingerprint with the host's sums */
+static int tables_compare(const ss_ctx_t *c, const unsigned long long fp[3])
+{
     if (fp[0] == c->fp_expect[0] && fp[1] == c->fp_expect[1] && fp[2] == c->fp_expect[2]) return SS_OK;
     fprintf(stderr, "[sniper_amd] device %d: the context's device tables no longer match the host's (%s%s%s differ)\n",
             c->device, fp[0] != c->fp_expect[0] ? "coef " : "", fp[1] != c->fp_expect[1] ? "lhet " : "",
             fp[2] != c->fp_expect[2] ? "fk/qAdd/prior/nt16/fast" : "");
     return SS_E_TABLES;
+}
+
+/* fingerprint the context's device tables and compare with the host's sums;
+ * the caller's stream order puts this after the upload / the launches it
+ * wants checked.  Synchronizes the context's stream. */
+static int tables_verify(ss_ctx_t *c)
+{
+    unsigned long long fp[3] = {0, 0, 0};
+    if (int rc = tables_fp_enqueue(c, fp)) return rc;
+    HIPCHK(hipStreamSynchronize(c->hstream));
+    return tables_compare(c, fp);
 }
 
 extern "C" void ss_ctx_destroy(ss_ctx_t *c)
@@ -480,17 +509,21 @@ static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
 
 /* The group kernel's fold-record buffers (SS_GRP_REC_BYTES per wave) for a
  * grid of `wgs` workgroups, allocated on first need and grown like the work
- * lists (the old buffers are retired, not reused, until ss_ctx_destroy): a
- * context that only ever scores small batches holds a few MB, not the
- * 403 MB of a full grid. */
+ * lists: by at least half each time, up to the full grid of n_cu workgroups
+ * (the old buffers are retired, not reused, until ss_ctx_destroy, so a run of
+ * slowly growing batches retires O(log n_cu) buffers, not one per batch).  A
+ * context that only ever scores small batches holds a few MB, not the 403 MB
+ * of a full grid. */
 static int ensure_grp_cap(ss_ctx_t *c, uint32_t wgs, hipStream_t s)
 {
     if (wgs <= c->grp_wgs) return SS_OK;
+    uint32_t want = std::max(wgs, c->grp_wgs + c->grp_wgs / 2);
+    want = std::max(std::min(want, (uint32_t)std::max(c->n_cu, 1)), wgs);
     dev_release(c, *(void **)&c->d_grp_rec, false);
     c->grp_wgs = 0;
-    if (int rc = dev_alloc(c, (void **)&c->d_grp_rec, (size_t)wgs * (SS_WIDE_BLOCK / 64) * SS_GRP_REC_BYTES, s))
+    if (int rc = dev_alloc(c, (void **)&c->d_grp_rec, (size_t)want * (SS_WIDE_BLOCK / 64) * SS_GRP_REC_BYTES, s))
         return rc;
-    c->grp_wgs = wgs;
+    c->grp_wgs = want;
     return SS_OK;
 }
 
@@ -752,6 +785,7 @@ extern "C" int ss_score_batch_host(ss_ctx_t *c, const ss_batch_t *b, const ss_ou
     const size_t o_cnt = off;   off = align_up(off + 16);
     const size_t o_calls = off; off = align_up(off + sizeof(ss_call_t) * (size_t)cap);
     const size_t o_glf = off;   off = align_up(off + (o->glf ? sizeof(ss_glf_t) * 2 * n : 0));
+    const size_t o_chk = off;   off = align_up(off + 32);     /* err word, table fingerprint */
     const size_t total = off;
     HIPCHK(hipSetDevice(c->device));
     int rc = ensure_stage(c, total);
@@ -791,9 +825,25 @@ extern "C" int ss_score_batch_host(ss_ctx_t *c, const ss_batch_t *b, const ss_ou
     HIPCHK(hipMemsetAsync(d + o_cnt, 0, 16, s));
     rc = ss_score_batch_device(c, &db, &dout, s);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h + o_sc, d + o_sc, total - o_sc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h + o_sc, d + o_sc, o_chk - o_sc, hipMemcpyDeviceToHost, s));
+    /* ss_ctx_check's work, queued behind the batch so that one synchronize
+     * serves both: the sticky error word and the table fingerprint */
+    HIPCHK(hipMemcpyAsync(h + o_chk, c->d_counters + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if ((rc = tables_fp_enqueue(c, reinterpret_cast<unsigned long long *>(h + o_chk + 8)))) return rc;
     HIPCHK(hipStreamSynchronize(s));
-    rc = ss_ctx_check(c);
+    {
+        uint32_t err;
+        unsigned long long fp[3];
+        memcpy(&err, h + o_chk, sizeof err);
+        memcpy(fp, h + o_chk + 8, sizeof fp);
+        rc = tables_compare(c, fp);
+        if (rc == SS_OK) rc = guards_check(c);
+        if (rc == SS_OK && err) {
+            HIPCHK(hipMemsetAsync(c->d_counters + 2, 0, sizeof(uint32_t), s));
+            HIPCHK(hipStreamSynchronize(s));
+            rc = (err & SS_KERR_MALFORMED) ? SS_E_INVAL : SS_E_CAPACITY;
+        }
+    }
     memcpy(o->score, h + o_sc, 4 * n);
     uint32_t ncalls, nclamp;
     memcpy(&ncalls, h + o_cnt, 4);

@@ -87,8 +87,8 @@ __device__ __forceinline__ double cr_sqrt(double d)
  * sums fk * q, f the same fk, q <= 63) and e * rcp(f) lies within a few ulp
  * (< 2^-16) of the correctly rounded quotient, so floor(q + 0.5) is exact
  * unless q + 0.5 falls within 2^-12 of an integer; those lanes (rare) take
- * the exact division in a wave-uniform branch.  f = 0 (a genotype without
- * other reads, whose index is unused) gives 4. */
+ * the exact division in a wave-uniform branch.  Callers pass f > 0 (a
+ * genotype without other reads passes 1: its index is unused). */
 __device__ __forceinline__ int bar_e_fast(float e, float f)
 {
     const float r = e * __builtin_amdgcn_rcpf(f) + 0.5f;
@@ -204,9 +204,10 @@ __device__ __forceinline__ void geno_p_range(uint32_t role, const float es[4], c
         }
         const bool hom = j == k;
         const uint32_t il = hom ? 0u : (c[j] << 8 | c[k]);
-        /* bar_e for every lane (no branch on c2: f = 0 gives a NaN quotient,
-         * which is not near an integer, and the index is not used) */
-        const uint32_t be = (uint32_t)bar_e_fast(e, f);
+        /* bar_e for every lane, no branch on c2; a lane with c2 = 0 (f = 0,
+         * its index unused) divides by 1 instead, so no inf / NaN reaches the
+         * float-to-int conversion (undefined in C++, poison in LLVM) */
+        const uint32_t be = (uint32_t)bar_e_fast(e, c2 ? f : 1.0f);
         const uint32_t ic = c2 ? (be << 16 | tot << 8 | c2) : 0u;
         lhv[t] = ss_tab_lhet(m)[il];
         cfv[t] = ss_tab_coef(m)[ic];

@@ -369,10 +369,19 @@ def test_stale_or_foreign_index_takes_streaming_walk(tmp_path):
     os.utime(dst / (t + ".bai"), ns=(st.st_atime_ns, st.st_mtime_ns - 10 ** 9))
     got, grouped = _grouped_dump(dst, fa, t, n)
     assert got == ref and not grouped
-    # written in the same second as its BAM (whole-second test, as htslib's): used
+    # an index stamped in whole seconds (a second-resolution copy) in the same
+    # second as its BAM (htslib's whole-second test): used
     sec = st.st_mtime_ns // 10 ** 9 * 10 ** 9
     os.utime(dst / t, ns=(st.st_atime_ns, sec + 5 * 10 ** 8))
     os.utime(dst / (t + ".bai"), ns=(st.st_atime_ns, sec))
+    got, grouped = _grouped_dump(dst, fa, t, n)
+    assert got == ref and grouped
+    # both stamped to the nanosecond: the BAM rewritten later in the same second
+    # as its index is refused; an index written after its BAM in that second is used
+    os.utime(dst / (t + ".bai"), ns=(st.st_atime_ns, sec + 2 * 10 ** 8))
+    got, grouped = _grouped_dump(dst, fa, t, n)
+    assert got == ref and not grouped
+    os.utime(dst / (t + ".bai"), ns=(st.st_atime_ns, sec + 7 * 10 ** 8))
     got, grouped = _grouped_dump(dst, fa, t, n)
     assert got == ref and grouped
     # foreign: the tumor BAM carries another dataset's index (same contig count)

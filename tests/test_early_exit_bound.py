@@ -2,8 +2,10 @@
 scores an all-reference site 255 without computing likelihoods when each
 sample has at least thr[n] reads of minq >= 24, thr from the host table
 (ss_capi.hip fast_table: the smallest c24 with
-24 * (fk[0] + .. + fk[c24 - 1]) * (1 - 1e-4) + min coef[q][n'][n'] >= 1 over
-q in [4, 63], n' <= n, enabled only with q_r >= 1).
+24 * (m[0] + .. + m[c24 - 1]) * (1 - 1e-4) + min coef[q][n'][n'] >= 1 over
+q in [4, 63], n' <= n, m[k] = min(fk[0 .. k]), enabled only with q_r >= 1).
+The running minimum keeps the bound sound when fk increases (theta > 1, which
+the reference's -T accepts: main.c:83 has no range check).
 
 This CPU test restates that table from the oracle's own model tables and
 checks the rule's soundness against the oracle (pinned to the compiled
@@ -22,8 +24,10 @@ def fast_thresholds(fk, coef, q_r):
     if q_r < 1:
         return thr
     F = np.zeros(130)
+    run_min = fk[0]
     for k in range(129):
-        F[k + 1] = F[k] + fk[min(k, 255)]
+        run_min = min(run_min, fk[min(k, 255)])
+        F[k + 1] = F[k] + run_min
     cm = 1e300
     for n in range(1, 129):
         cm = min(cm, min(coef[q << 16 | n << 8 | n] for q in range(4, 64)))
@@ -35,12 +39,15 @@ def fast_thresholds(fk, coef, q_r):
 
 
 def _sample(pkg, base, n, c24, rest_bq, alternate):
-    reads = [pkg.pack_read(60, 24, base, 0) for _ in range(c24)]
+    # alternating strands give the q-24 reads the weights fk[0], fk[0], fk[1],
+    # fk[1], ...: the smallest ones when fk increases (theta > 1)
+    reads = [pkg.pack_read(60, 24, base, (i & 1) if alternate else 0) for i in range(c24)]
     reads += [pkg.pack_read(60, rest_bq, base, (i & 1) if alternate else 0) for i in range(n - c24)]
     return reads
 
 
-@pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"]])
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"],
+                                  ["-T", "1.2"]])
 def test_early_exit_thresholds_sound(pkg, oracle, opts):
     o = oracle.Oracle(oracle.opts_to_params(list(opts)))
     t = o.tables()

@@ -452,7 +452,8 @@ def all_reference_sites(pkg):
     return s
 
 
-@pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"]])
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"],
+                                  ["-T", "1.2"]])
 def test_all_reference_sites_parity(pkg, oracle, opts):
     """all_reference_sites against the oracle, with and without glf records,
     plus 60x/30x and 30x/25x batches with few errors (most sites
@@ -483,7 +484,7 @@ def test_early_exit_mixed_blocks(pkg, oracle, opts):
     assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), opts)
 
 
-@pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"]])
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"], ["-T", "1.2"]])
 def test_all_reference_sites_match_real_reference(pkg, tmp_path, opts):
     """all_reference_sites through the compiled reference on THIS machine vs
     the GPU (no glf records requested)."""
