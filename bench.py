@@ -280,10 +280,14 @@ def live_counters(args, kernel="ss_score_main"):
     if env.get("SNIPER_AMD_LIB"):                  # the child runs in /tmp: the library the bench loaded
         env["SNIPER_AMD_LIB"] = os.path.abspath(env["SNIPER_AMD_LIB"])
     vals = {}
-    for counters in PMC_PASSES:
+    # the counter passes, then one --kernel-trace pass over the same child: the
+    # dispatches' own durations next to the bench's HIP-event times (the
+    # rocprofv3 --stats average includes each batch's cold first launch)
+    for counters in PMC_PASSES + (None,):
         out = tempfile.mkdtemp(prefix="ss_pmc_", dir="/tmp")
         try:
-            cmd = [exe, "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "run", "--",
+            mode = ["--kernel-trace", "--stats"] if counters is None else ["--pmc", *counters]
+            cmd = [exe, *mode, "--output-format", "csv", "-d", out, "-o", "run", "--",
                    sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
                    *(["--c4-scale", str(args.c4_scale)] if args.c4_scale is not None else []),
                    "--chunk", str(args.chunk), "--sites", str(args.sites),
@@ -302,9 +306,27 @@ def live_counters(args, kernel="ss_score_main"):
                 raise
             r = subprocess.CompletedProcess(cmd, proc.returncode, "", err)
             path = None
+            want = "run_kernel_trace.csv" if counters is None else "run_counter_collection.csv"
             for dp, _, fs in os.walk(out):
-                if "run_counter_collection.csv" in fs:
-                    path = os.path.join(dp, "run_counter_collection.csv")
+                if want in fs:
+                    path = os.path.join(dp, want)
+            if counters is None and r.returncode == 0 and path is not None:
+                durs = []
+                with open(path) as f:
+                    for row in csv.DictReader(f):
+                        if re.search(re.escape(kernel) + r"[<(]", row["Kernel_Name"]):
+                            durs.append((int(row["Dispatch_Id"]),
+                                         float(row["End_Timestamp"]) - float(row["Start_Timestamp"])))
+                durs = [d for _, d in sorted(durs)]
+                n_pass = len(durs) // max(1, args.pmc_launches)
+                warm = durs[n_pass:] or durs
+                vals["_kt"] = {"all_dispatches_ms": round(float(np.mean(durs)) / 1e6, 4) if durs else None,
+                               "warm_dispatches_ms": round(float(np.mean(warm)) / 1e6, 4) if warm else None,
+                               "dispatches": len(durs), "cold_dropped": n_pass}
+                continue
+            if counters is None:            # the trace is a side figure: its failure drops only it
+                print(f"bench: kernel-trace pass failed (rc {r.returncode}): {r.stderr[-300:]}", file=sys.stderr)
+                continue
             if r.returncode != 0 or path is None:
                 print(f"bench: PMC pass {counters} failed (rc {r.returncode}): {r.stderr[-500:]}", file=sys.stderr)
                 return None
@@ -829,6 +851,14 @@ def main():
                           "per-launch means of the second pass",
             }
             rf["pmc_launch_world"] = world
+            if pc.get("_kt"):
+                # `frac` uses the HIP-event mean of the timed
+                # launches (the same launches as `value`); rocprofv3's trace of
+                # the counter child's launches is quoted beside it
+                rf["kernel_ms_rocprof_trace"] = dict(pc["_kt"], hip_events_ms=rf["avg_kernel_ms"],
+                                                     source="rocprofv3 --kernel-trace over the counter child "
+                                                            "(its first launch per batch is cold and dropped "
+                                                            "from warm_dispatches_ms)")
     if rank == 0 and not args.no_host_fed:
         result["host_fed"] = host_fed(ctx, pkg, args, dev)
     if rank == 0 and not args.no_cpu:

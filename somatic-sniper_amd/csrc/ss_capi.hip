@@ -51,6 +51,7 @@ struct ss_ctx {
     /* work lists */
     uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6..7] listed
                                  entries | segments << 32, [8] the group kernel's chunk counter,
+                                 [9] the deep kernel's chunk counter, [10] deep3 count,
                                  [16..21] the table fingerprint (3 x u64) */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
@@ -487,8 +488,9 @@ extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double
     return SS_OK;
 }
 
-/* the deep list buffer holds two lists of deep_cap entries: the main
- * kernel's per-wave segments (deep) and the group kernel's overflow (deep2).
+/* the deep list buffer holds three lists of deep_cap entries: the main
+ * kernel's per-wave segments (deep), the group kernel's overflow (deep2) and
+ * the deep kernel's (deep3).
  * Grown for a batch larger than any before (by at least half, so a run of
  * growing batches allocates O(log) times); the old list may still be read by
  * the context's previous launch, so it is retired, not reused, until
@@ -502,7 +504,7 @@ static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
     if (cap < n_sites) return SS_E_INVAL;
     dev_release(c, *(void **)&c->d_deep_list, false);
     c->deep_cap = 0;
-    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 2 * cap * sizeof(uint32_t), s)) return rc;
+    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 3 * cap * sizeof(uint32_t), s)) return rc;
     c->deep_cap = (uint32_t)cap;
     return SS_OK;
 }
@@ -559,9 +561,9 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     const uint64_t wg_need = (grp_chunks_max + SS_WIDE_BLOCK / 64 - 1) / (SS_WIDE_BLOCK / 64);
     const int wide_grid = (int)std::min<uint64_t>((uint64_t)c->n_cu, wg_need);
     if ((rc = ensure_grp_cap(c, (uint32_t)wide_grid, s))) return rc;
-    /* counters: deep2, listed segments and entries, the group kernel's next
-     * chunk (err is sticky until ss_ctx_check) */
-    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 4 * sizeof(uint32_t), s));
+    /* counters: deep2, listed segments and entries, the group and deep
+     * kernels' next chunks, deep3 (err is sticky until ss_ctx_check) */
+    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 6 * sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
     memset(&a, 0, sizeof(a));
@@ -585,6 +587,9 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.deep_cap = c->deep_cap;
     a.deep2_list = c->d_deep_list + c->deep_cap;
     a.deep2_count = c->d_counters + 5;
+    a.deep_next = c->d_counters + 9;
+    a.deep3_list = c->d_deep_list + 2 * (size_t)c->deep_cap;
+    a.deep3_count = c->d_counters + 10;
     a.deep_acc = reinterpret_cast<unsigned long long *>(c->d_counters + 6);   /* 8-byte aligned */
     a.wide_next = c->d_counters + 8;
     a.grp_rec = c->d_grp_rec;
@@ -598,7 +603,8 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.m.min_somatic_qual = c->hm.prm.min_somatic_qual;
     a.m.flags = (c->hm.prm.use_joint_priors ? SS_MF_JOINT : 0u) | (c->hm.prm.include_loh ? SS_MF_LOH : 0u) |
                 (c->hm.prm.include_gor ? SS_MF_GOR : 0u) | (c->fast_ok ? SS_MF_FAST : 0u);
-    const int deep_grid = c->n_cu * 3;              /* 3 blocks (12 one-site waves) per CU: LDS */
+    const int deep_grid = c->n_cu;                  /* one 8-wave block per CU: LDS */
+    const int wild_grid = c->n_cu * 3;              /* 3 blocks (12 one-site waves) per CU: LDS */
     c->last_stream = s;
     const hipEvent_t *evs = nullptr;
     if (c->timing && c->n_logged < 4096) {
@@ -610,7 +616,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         evs = c->ev->data() + SS_EV_PER_LAUNCH * c->n_logged;
         ++c->n_logged;
     }
-    int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, s, evs);
+    int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, wild_grid, s, evs);
     if (e != 0) return SS_E_HIP;
     HIPCHK(hipEventRecord(c->done, s));
     c->launched = 1;

@@ -73,9 +73,13 @@ struct ss_score_args {
     uint32_t  *wide_next;     /* the group kernel's next chunk of GB listed entries (zeroed per launch) */
     uint32_t   deep_seg_cap;
     uint32_t   deep_nseg;     /* = main-kernel waves */
-    uint32_t   deep_cap;      /* deep2 list capacity (>= n_sites: cannot overflow) */
+    uint32_t   deep_cap;      /* deep2 / deep3 list capacity (>= n_sites: cannot overflow) */
     uint32_t  *deep2_list;    /* sites the group kernel cannot sort, any depth (ss_score_deep) */
     uint32_t  *deep2_count;
+    uint32_t  *deep_next;     /* ss_score_deep's next chunk of deep2 entries (zeroed per launch) */
+    uint32_t  *deep3_list;    /* sites ss_score_deep hands on (ss_score_wild): a read of minq >= 64,
+                                 a sample past SS_BINS_MAXN reads, malformed offsets */
+    uint32_t  *deep3_count;
     uint32_t  *err;           /* sticky error bits, see SS_KERR_* */
     uint8_t   *grp_rec;       /* the group kernel's fold records: SS_GRP_REC_BYTES per wave */
     ss_dev_model m;
@@ -89,18 +93,23 @@ struct ss_score_args {
 #define SS_MAIN_SITES      64    /* sites per main-kernel wave block           */
 #define SS_MAIN_GRID_PER_CU 128  /* main-kernel workgroups per CU: 3 resident (166 VGPRs, 52.5 KB LDS each),
                                     the rest queued as short-lived waves (+5.5% over 16 per CU) */
-#define SS_DEEP_BLOCK      256
+#define SS_DEEP_BLOCK      512   /* 8 waves, one workgroup per CU (LDS: 19 KB per wave) */
+#define SS_WILD_BLOCK      256   /* 4 one-site waves per workgroup, 3 per CU (LDS) */
+#define SS_BINS_MAXN       65535u /* reads per sample ss_score_deep takes (16-bit bin counts) */
 #ifndef SS_WIDE_BLOCK
 #define SS_WIDE_BLOCK      768   /* 12 waves, one workgroup per CU (168 VGPRs: 3 waves per SIMD) */
 #endif
-#define SS_WIDE_MAXSLOTS   2048  /* sort slots (tumor + pad + normal) per site    */
+#ifndef SS_WIDE_MAXSLOTS
+#define SS_WIDE_MAXSLOTS   2048  /* reads per sample the group kernel sorts (A/B builds may lower it) */
+#endif
 #define SS_GRP_REC_MAX     131072 /* fold-record bytes of one group-kernel chunk: 32 sites x 2 x 2048 */
 #define SS_GRP_REC_PAD     64    /* pad before and after (a 16-record window may reach past either end) */
 #define SS_GRP_REC_BYTES   (SS_GRP_REC_MAX + 2 * SS_GRP_REC_PAD)
 
 /* Launchers (return hipError_t as int). */
-int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, hipStream_t s,
-                    const hipEvent_t *ev /* 4 events (before main, after main, after wide, after deep) or null */);
+int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, int wild_grid,
+                    hipStream_t s,
+                    const hipEvent_t *ev /* 4 events (before main, after main, after wide, after deep + wild) or null */);
 /* out3 (zeroed by the caller): fingerprint sums of coef, lhet and the rest (ss_host.h) */
 int ss_launch_tab_fingerprint(const uint8_t *tab, unsigned long long *out3, hipStream_t s);
 int ss_launch_synth_depth(const ss_synth_k_t &k, uint64_t first, uint64_t n, uint8_t *ref,

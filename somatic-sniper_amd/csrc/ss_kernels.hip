@@ -2031,8 +2031,10 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
 }
 
 /* --------------------------------------------------------------------------
- * Deep kernel: the sites the group kernel cannot sort (more than
- * SS_WIDE_MAXSLOTS sort slots, any depth) and sites with malformed offsets.
+ * Wild kernel (ss_score_wild, the deep kernel of rounds 1-5): the sites the
+ * deep kernel (below) hands on -- a read of minq >= 64 (bins past the bottom
+ * window), a sample of more than SS_BINS_MAXN reads, malformed offsets.  Any
+ * depth, any quality.
  *
  * No sort: the fold only needs each (sample, base) group's reads in the
  * reference's descending key order (sniper_maqcns.c:157-172), and reads with
@@ -2059,7 +2061,7 @@ namespace {
 #define DW_BINS 368                     /* bins per group in one LDS window */
 #define DW_HIST (8 * DW_BINS)
 #define DW_OCC (DW_HIST / 32)
-#define DEEP_WAVES (SS_DEEP_BLOCK / 64)
+#define DEEP_WAVES (SS_WILD_BLOCK / 64)
 static_assert(DW_HIST % 32 == 0 && DW_BINS % 4 == 0, "bitmap words");
 
 struct alignas(16) DeepWave {
@@ -2189,7 +2191,7 @@ __device__ __forceinline__ void deep_fold(const uint32_t *hist, const uint32_t *
 
 }  // namespace
 
-__global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
+__global__ __launch_bounds__(SS_WILD_BLOCK) void ss_score_wild(ss_score_args a)
 {
     __shared__ double fk[256];
     __shared__ DeepWave DW[DEEP_WAVES];
@@ -2199,7 +2201,7 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
     __syncthreads();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     DeepWave &D = DW[wv];
-    const uint32_t count = *a.deep2_count;
+    const uint32_t count = *a.deep3_count;
     const uint32_t lim = count < a.deep_cap ? count : a.deep_cap;
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
@@ -2209,7 +2211,7 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
         /* arguments re-read from the kernarg segment where used: they do not
          * stay live in SGPRs across the site loop (44 SGPR spills before) */
         const ss_score_args &k = kernarg_args();
-        const uint32_t s = k.deep2_list[w];
+        const uint32_t s = k.deep3_list[w];
         const uint32_t ot = k.off_t[s], ot1 = k.off_t[s + 1], on = k.off_n[s], on1 = k.off_n[s + 1];
         if (!site_wellformed(ot, ot1, end_t) || !site_wellformed(on, on1, end_n)) {
             if (lane == 0) {
@@ -2297,6 +2299,419 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
 }
 
 /* --------------------------------------------------------------------------
+ * Deep kernel (round 6): the group kernel's overflow list -- sites with a
+ * sample past SS_WIDE_MAXSLOTS reads, and the ones it routes on (a read of
+ * minq >= 64, malformed offsets: this kernel passes those to ss_score_wild,
+ * with samples past SS_BINS_MAXN reads).
+ *
+ * Counting sort, as ss_score_wild, but with the work laid out for 64 lanes:
+ *   1. per site (the whole wave): each sample's reads are counted into a
+ *      16-bit histogram of order bins in LDS (ds_add, eight loads in flight
+ *      per lane); slots per sample: group A the deep bins 0..367 (hasbase
+ *      orders A before N / IUPAC reads there), C / G / T the same bins without
+ *      the hasbase bit (always 1), 184 each -- 960 slots in all.  The
+ *      histogram then becomes runs (q | strand << 6 | count << 7, count <=
+ *      511) in the reference's walk order -- per group, descending key -- by
+ *      ballot compaction, 64 slots per row, appended to the wave's run list;
+ *   2. per round of up to 32 sites (when the run list or the round is full):
+ *      lane = (site, sample) folds its unit's four group chains from its runs
+ *      (the largest group first), one read per step with fk[w] from LDS --
+ *      the reference's serial float chains, every lane busy -- then evaluates
+ *      the ten genotypes, and lane = site decides.
+ * Rounds 1-5 folded one site per wave with 16 of 64 lanes (ss_score_wild):
+ * 33,000 VALU instructions per site at 3000x/3000x, 0.045 of the HBM roofline.
+ * ------------------------------------------------------------------------ */
+namespace {
+
+#define BN_WAVES (SS_DEEP_BLOCK / 64)
+#define BN_SLOTS 640                    /* bin slots per sample: group A 256, C / G / T 128 each */
+#define BN_WORDS (BN_SLOTS / 2)         /* 16-bit counts, two per word */
+#define BN_ROWS (BN_SLOTS / 64)         /* compaction rows: A 0..3, C 4..5, G 6..7, T 8..9 */
+#define BN_SITES 32                     /* sites per fold round: lane = (site, sample) */
+#define BN_CHUNK 16                     /* list entries a wave draws at a time */
+#define BN_ENT_CAP 6384                 /* runs per wave: a whole site always fits an empty list */
+#define BN_FK_ZERO 256
+static_assert(BN_ENT_CAP >= 2 * (BN_SLOTS + SS_BINS_MAXN / 511 + 1), "a site's runs fit an empty list");
+
+struct alignas(16) BinsLds {
+    uint32_t hist[2][BN_WORDS];          /* tumor, normal: slot s = 16-bit half s & 1 of word s >> 1 */
+    uint2    slut[2][32];                /* per sample, read nt16 | strand << 4: histogram byte offset << 8 |
+                                            log2(bytes per minq), and the count's half (1 << 16 strand) */
+    uint16_t ent[BN_ENT_CAP];            /* runs: q | strand << 6 | count << 7 */
+    uint16_t u_gs[2 * BN_SITES][6];      /* unit: first run of groups 0..3, then the unit's end */
+    uint32_t u_cnt[2 * BN_SITES][4];     /* unit: contributing reads per group */
+    uint32_t u_rms[2 * BN_SITES];        /* unit: rms sum (< 2^16 reads x 3600) */
+    uint32_t u_n[2 * BN_SITES];          /* unit: non-deleted depth */
+    uint32_t s_site[BN_SITES];
+    uint32_t s_refc[BN_SITES];           /* ref char | nt16 << 8 */
+    SlotRes  res[2 * BN_SITES];
+};
+
+/* Histogram slots of one sample.  A read of minq < 64 whose clamped q is > 0
+ * (sniper_maqcns.c:165-166) counts in
+ *   group A (base 0):   4 minq + 2 hasbase + strand       (256 slots)
+ *   group C, G, T:      gb + 2 minq + strand, gb = 128 (base + 1), hasbase = 1
+ * and the fold walks a group from its top slot down: the reference's
+ * descending key order (:144-157) up to swaps of reads with equal (q, strand).
+ * For minq < 4 the key's baseQ bits order reads further (E = baseQ >> 6 and
+ * baseQ & 0x3f != 0 set q, deep_bin); with baseQ < 64 they are all q = 4 and
+ * need no more slots.  A read of minq >= 64, or of minq < 4 and baseQ >= 64,
+ * sends its site to ss_score_wild (never produced by short-read aligners). */
+__device__ __forceinline__ uint32_t bn_gbase(uint32_t g) { return g ? 128u * (g + 1u) : 0u; }
+
+/* the per-sample lookup rows for a site of reference code ref16: lane =
+ * sample << 5 | strand << 4 | read nt16 (bam_nt16_nt4_table semantics,
+ * :153-154: '=' is the reference, N / IUPAC count as A without hasbase) */
+__device__ __forceinline__ void bn_slut_build(BinsLds &B, uint32_t ref16)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t smp = lane >> 5, st = (lane >> 4) & 1u, nt16 = lane & 15u;
+    const uint32_t code = nt16 ? nt16 : ref16;
+    const uint32_t nt4 = code == 1u ? 0u : code == 2u ? 1u : code == 4u ? 2u : code == 8u ? 3u : 4u;
+    const uint32_t hb = nt4 < 4u ? 1u : 0u, base = hb ? nt4 : 0u;
+    /* byte offset of minq 0's word in the sample's histogram: A 4 hasbase,
+     * else 2 gb; bytes per minq: A 8, else 4 */
+    const uint32_t wb = base ? 2u * bn_gbase(base) : 4u * hb;
+    B.slut[smp][lane & 31u] = make_uint2(wb << 8 | (base ? 2u : 3u), 1u << (16u * st));
+}
+
+/* run code (q | strand << 6) of a slot of group g: q = max(minq, 4) */
+__device__ __forceinline__ uint32_t bn_code(uint32_t slot, uint32_t g)
+{
+    const uint32_t minq = g ? (slot - bn_gbase(g)) >> 1 : slot >> 2;
+    return max(minq, 4u) | (slot & 1u) << 6;
+}
+
+/* one sample's reads into its (zeroed) histogram, eight loads in flight per
+ * lane (their index clamped to the last read, so no load is predicated);
+ * adds the rms terms (:173-174) to rs; true when a read needs ss_score_wild */
+__device__ __forceinline__ bool bn_pass(const uint32_t *reads, uint32_t n, const uint2 *slut, uint32_t cap,
+                                        uint32_t *hist, uint32_t &rs)
+{
+    const uint32_t lane = lane_id();
+    bool wild = false;
+    char *hb = reinterpret_cast<char *>(hist);
+    for (uint32_t i0 = 0; i0 < n; i0 += 8u * 64u) {
+        uint32_t rd[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) rd[j] = __builtin_nontemporal_load(reads + min(i0 + lane + j * 64u, n - 1u));
+        /* the eight lookups first, then the addresses (pinned in registers:
+         * the compiler would otherwise sink each lookup into its atomic's
+         * branch and wait for it there), then the atomics */
+        uint32_t x[8], addr[8], val[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) {
+            x[j] = i0 + lane + j * 64u < n ? rd[j] : 0u;      /* 0: no contribution, no rms */
+            const uint2 e = slut[(x[j] >> 16) & 31u];
+            addr[j] = e.x;
+            val[j] = e.y;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) {
+            const uint32_t minq = min(x[j] & 0xffu, (x[j] >> 8) & 0xffu);
+            addr[j] = (addr[j] >> 8) + (minq << (addr[j] & 31u));
+            asm volatile("" : "+v"(addr[j]), "+v"(val[j]));
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) {
+            const uint32_t bq = (x[j] >> 8) & 0xffu;
+            const uint32_t minq = min(x[j] & 0xffu, bq);
+            const uint32_t t = min(x[j] & 0x7fu, cap);
+            rs += t * t;
+            const bool w = minq >= 64u || (minq < 4u && bq >= 64u);
+            wild |= w;
+            if (bq != 0u && !w) atomicAdd(reinterpret_cast<uint32_t *>(hb + addr[j]), val[j]);
+        }
+    }
+    return wild;
+}
+
+/* a unit's histogram as runs in the fold's walk order -- groups A, C, G, T,
+ * each from its top slot down (the reference's descending key walk) --
+ * appended at ent[pos ..] (writes stop at BN_ENT_CAP; the caller checks the
+ * returned end); the groups' first runs go to gs[0..3], the end to gs[4],
+ * their contributing reads to cnt[0..3] (wave-uniform); returns the new end.
+ * Row r holds walk positions 64 r + lane. */
+__device__ __forceinline__ uint32_t bn_runs(const uint32_t *hist, uint16_t *ent, uint32_t pos, uint32_t (&gs)[5],
+                                            uint32_t (&cnt)[4])
+{
+    const uint32_t lane = lane_id();
+    const uint16_t *h16 = reinterpret_cast<const uint16_t *>(hist);
+    uint32_t part = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < BN_ROWS; ++r) {
+        const uint32_t g = r < 4u ? 0u : (r - 2u) >> 1;
+        const uint32_t r0 = g ? 2u * g + 2u : 0u;            /* the group's first row */
+        const uint32_t gb = bn_gbase(g), gsz = g ? 128u : 256u;
+        if (r == r0) gs[g] = pos;
+        const uint32_t slot = gb + gsz - 1u - (64u * (r - r0) + lane);
+        const uint32_t c = h16[slot];
+        const uint32_t code = bn_code(slot, g);
+        if (!__ballot(c > 511u)) {
+            const uint64_t m = __ballot(c != 0u);
+            const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (c && pos + off < BN_ENT_CAP) ent[pos + off] = (uint16_t)(code | c << 7);
+            pos += (uint32_t)__popcll(m);
+        } else {                                   /* a bin of more than 511 reads: several runs */
+            const uint32_t ne = (c + 510u) / 511u;
+            const uint32_t incl = wave_scan(ne);
+            uint32_t o = pos + incl - ne;
+            for (uint32_t left = c; left;) {
+                const uint32_t x = min(left, 511u);
+                if (o < BN_ENT_CAP) ent[o] = (uint16_t)(code | x << 7);
+                ++o;
+                left -= x;
+            }
+            pos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        part += c;
+        if (r == 3u || r == 5u || r == 7u || r == 9u) {
+            cnt[g] = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(part), 63);
+            part = 0;
+        }
+    }
+    gs[4] = pos;
+    return pos;
+}
+
+/* one group chain of a unit from its runs ent[e0 ..] (T reads), one read per
+ * step: e = (float)((double)e + fk[w] * q), f = (float)((double)f + fk[w])
+ * (sniper_maqcns.c:167-170) with per-strand w counters (16-bit fields of W,
+ * saturated at 255 where used).  The wave steps to its longest chain; a lane
+ * past its own reads adds fk's zero entry (x + 0.0 == x).  Software
+ * pipelined: step t + 1 is decoded and its fk[w] read from LDS before step
+ * t's float arithmetic, so the LDS latency hides under it. */
+struct BnCur {
+    uint32_t rem, q, sh, ptr, nxt;
+};
+
+/* decode step t of a chain (advancing to the next run when the current one
+ * is used up) and return its fk index */
+__device__ __forceinline__ uint32_t bn_step_idx(const uint16_t *ent, BnCur &c, uint32_t W, uint32_t t, uint32_t T)
+{
+    const bool live = t < T;
+    const bool take = c.rem == 0u && live;
+    c.q = take ? (c.nxt & 63u) : c.q;
+    c.sh = take ? ((c.nxt >> 2) & 16u) : c.sh;          /* strand << 4 */
+    c.rem = take ? (c.nxt >> 7) : c.rem;
+    c.ptr += take ? 1u : 0u;
+    c.nxt = ent[c.ptr];
+    c.rem -= live ? 1u : 0u;
+    const uint32_t w = __builtin_amdgcn_ubfe(W, c.sh, 16u);
+    return live ? min(w, 255u) : (uint32_t)BN_FK_ZERO;
+}
+
+__device__ __forceinline__ void bn_chain(const uint16_t *ent, uint32_t e0, uint32_t T, const double *fk, float &e,
+                                         float &f)
+{
+    e = 0.0f;
+    f = 0.0f;
+    const uint32_t Tm = wave_max(T);
+    if (Tm == 0u) return;
+    BnCur c = {0u, 0u, 0u, e0, ent[e0]};
+    uint32_t W = 0;
+    double fv = fk[bn_step_idx(ent, c, W, 0u, T)];
+    uint32_t qc = c.q, shc = c.sh;
+    for (uint32_t t = 0; t < Tm; ++t) {
+        W += 1u << shc;                                     /* step t's strand counter */
+        const double fvn = fk[bn_step_idx(ent, c, W, t + 1u, T)];
+        e = (float)((double)e + fv * (double)qc);
+        f = (float)((double)f + fv);
+        fv = fvn;
+        qc = c.q;
+        shc = c.sh;
+    }
+}
+
+/* fold, likelihoods, quantisation and the decision for the round's sites.
+ * Inlined at its one call site: kernarg_args() reads the kernel's argument
+ * segment, whose pointer a called (not inlined) function does not have. */
+__device__ __forceinline__ void bn_round(BinsLds &B, uint32_t nsite, const double *fk, const int16_t *qtab)
+{
+    const ss_score_args &a = kernarg_args();
+    const uint32_t lane = lane_id();
+    const bool act = lane < 2u * nsite;
+    const uint32_t u = act ? lane : 0u;
+    uint32_t cnt[4], gs[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        cnt[g] = act ? B.u_cnt[u][g] : 0u;
+        gs[g] = B.u_gs[u][g];
+    }
+    uint32_t L = 0;
+#pragma unroll
+    for (uint32_t b = 1; b < 4; ++b) L = cnt[b] > (L == 0 ? cnt[0] : (L == 1 ? cnt[1] : cnt[2])) ? b : L;
+    float es[4], fs[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        /* the largest group first, then the other three */
+        const uint32_t g = i == 0 ? L : (i - 1u) + ((i - 1u) >= L ? 1u : 0u);
+        const uint32_t e0 = g == 0 ? gs[0] : (g == 1 ? gs[1] : (g == 2 ? gs[2] : gs[3]));
+        const uint32_t T = g == 0 ? cnt[0] : (g == 1 ? cnt[1] : (g == 2 ? cnt[2] : cnt[3]));
+        float e, f;
+        bn_chain(B.ent, e0, T, fk, e, f);
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b)
+            if (b == g) { es[b] = e; fs[b] = f; }
+    }
+    uint32_t c[4];
+    const uint32_t tot = rescale_counts(cnt, c);
+    float p[10];
+    geno_p5(0u, es, fs, c, tot, a.m, p);
+    geno_p5(1u, es, fs, c, tot, a.m, p + 5);
+    if (act) {
+        const uint32_t n = B.u_n[u];
+        uint32_t lk[10], min_lk, rms_q, cns;
+        glf_finish(p, es, n, B.u_rms[u], a.m, lk, min_lk, rms_q, cns);
+        SlotRes &r = B.res[u];
+        uint32_t *rw = reinterpret_cast<uint32_t *>(r.lk);
+        rw[0] = lk[0] | lk[1] << 8 | lk[2] << 16 | lk[3] << 24;
+        rw[1] = lk[4] | lk[5] << 8 | lk[6] << 16 | lk[7] << 24;
+        rw[2] = lk[8] | lk[9] << 8;
+        r.cns = cns;
+        r.depth = n;
+        if (a.glf) {
+            const uint32_t sl = u >> 1;
+            store_glf(&a.glf[2ull * B.s_site[sl] + (u & 1u)], B.s_refc[sl] >> 8, lk, min_lk, rms_q, n);
+        }
+    }
+    wave_sync();
+    if (lane < nsite) decide_site(a, qtab, B.s_site[lane], B.s_refc[lane], B.res[2u * lane], B.res[2u * lane + 1u]);
+    wave_sync();
+}
+
+/* a counted site's units (its runs are written) as round slot i */
+__device__ __forceinline__ void bn_unit_info(BinsLds &B, uint32_t i, uint32_t s, uint32_t refc, uint32_t ref16,
+                                             uint32_t nt, uint32_t nn, uint32_t rts, uint32_t rns,
+                                             const uint32_t (&gsT)[5],
+                                             const uint32_t (&gsN)[5], const uint32_t (&cT)[4],
+                                             const uint32_t (&cN)[4])
+{
+    if (lane_id() == 0u) {
+        const uint32_t uT = 2u * i, uN = uT + 1u;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            B.u_gs[uT][g] = (uint16_t)gsT[g];
+            B.u_gs[uN][g] = (uint16_t)gsN[g];
+            B.u_cnt[uT][g] = cT[g];
+            B.u_cnt[uN][g] = cN[g];
+        }
+        B.u_gs[uT][4] = (uint16_t)gsT[4];
+        B.u_gs[uN][4] = (uint16_t)gsN[4];
+        B.u_rms[uT] = rts;
+        B.u_rms[uN] = rns;
+        B.u_n[uT] = nt;
+        B.u_n[uN] = nn;
+        B.s_site[i] = s;
+        B.s_refc[i] = refc | ref16 << 8;
+    }
+    wave_sync();
+}
+
+/* hand a site on to ss_score_wild */
+__device__ __forceinline__ void bn_to_wild(uint32_t s)
+{
+    const ss_score_args &k = kernarg_args();
+    if (lane_id() == 0u) {
+        const uint32_t d = atomicAdd(k.deep3_count, 1u);
+        if (d < k.deep_cap) k.deep3_list[d] = s;
+        else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
+    }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
+{
+    __shared__ double fk[BN_FK_ZERO + 1];
+    __shared__ int16_t qtab[1024];                  /* qAddTable, as in ss_score_main */
+    __shared__ BinsLds BL[BN_WAVES];
+    const uint32_t count0 = *a.deep2_count;
+    const uint32_t count = count0 < a.deep_cap ? count0 : a.deep_cap;
+    if (count == 0u) return;
+    for (uint32_t i = threadIdx.x; i <= BN_FK_ZERO; i += blockDim.x) fk[i] = i < 256u ? ss_tab_fk(a.m)[i] : 0.0;
+    for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) qtab[i] = (int16_t)ss_tab_qadd(a.m)[i];
+    __syncthreads();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    BinsLds &B = BL[wv];
+    const uint32_t lane = lane_id();
+    uint32_t cur = 0, cend = 0;                     /* the wave's current list entries (uniform) */
+    uint32_t nsite = 0, nent = 0;                   /* the current round */
+    bool end = false;
+    /* the site whose histograms are built (s, depths, reference, rms sums) */
+    uint32_t s = 0, nt = 0, nn = 0, refc = 0, ref16 = 0;
+    uint32_t rts = 0, rns = 0;
+    /* one bn_round call site: each iteration fetches and counts a site, writes
+     * its runs when they fit the round, and folds the round when it is full,
+     * when the site's runs did not fit (they are written again behind the
+     * folded round: the histograms stay), or at the end of the list */
+    for (;;) {
+        bool ready = false;
+        if (!end && cur == cend) {
+            uint32_t ch = 0;
+            if (lane == 0u) ch = atomicAdd(kernarg_args().deep_next, 1u);
+            cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * BN_CHUNK;
+            end = cur >= count;
+            cend = end ? cur : min(cur + BN_CHUNK, count);
+        }
+        if (!end) {
+            const ss_score_args &k = kernarg_args();
+            s = k.deep2_list[cur++];
+            const uint32_t ot = k.off_t[s], ot1 = k.off_t[s + 1], on = k.off_n[s], on1 = k.off_n[s + 1];
+            const uint32_t end_t = k.off_t[k.n_sites], end_n = k.off_n[k.n_sites];
+            if (!site_wellformed(ot, ot1, end_t) || !site_wellformed(on, on1, end_n) || ot1 - ot > SS_BINS_MAXN ||
+                on1 - on > SS_BINS_MAXN) {
+                bn_to_wild(s);                         /* it reports malformed offsets (-2) */
+                continue;
+            }
+            nt = ot1 - ot;
+            nn = on1 - on;
+            refc = k.ref[s];
+            ref16 = ss_tab_nt16(k.m)[refc];
+            bn_slut_build(B, ref16);
+            {
+                uint4 *h4 = reinterpret_cast<uint4 *>(&B.hist[0][0]);
+                for (uint32_t i = lane; i < BN_WORDS / 2u; i += 64u) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+            }
+            wave_sync();
+            const uint32_t cap = (uint32_t)k.m.cap_mapQ;
+            uint32_t rt = 0, rn = 0;
+            bool wild = bn_pass(k.reads_t + ot, nt, B.slut[0], cap, B.hist[0], rt);
+            wild |= bn_pass(k.reads_n + on, nn, B.slut[1], cap, B.hist[1], rn);
+            if (__ballot(wild)) {                      /* ss_score_wild's windows and baseQ bins */
+                bn_to_wild(s);
+                continue;
+            }
+            rts = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(rt), 63);   /* rms sums over the wave */
+            rns = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(rn), 63);
+            wave_sync();
+            ready = true;
+        }
+        uint32_t gsT[5], gsN[5], cT[4], cN[4];
+        if (ready && nsite < BN_SITES) {
+            const uint32_t e2 = bn_runs(B.hist[1], B.ent, bn_runs(B.hist[0], B.ent, nent, gsT, cT), gsN, cN);
+            if (e2 <= BN_ENT_CAP) {
+                bn_unit_info(B, nsite, s, refc, ref16, nt, nn, rts, rns, gsT, gsN, cT, cN);
+                ++nsite;
+                nent = e2;
+                ready = false;
+            }
+        }
+        if (ready || nsite == BN_SITES || (end && nsite)) {
+            bn_round(B, nsite, fk, qtab);
+            nsite = 0;
+            nent = 0;
+            if (ready) {
+                nent = bn_runs(B.hist[1], B.ent, bn_runs(B.hist[0], B.ent, 0u, gsT, cT), gsN, cN);
+                bn_unit_info(B, 0u, s, refc, ref16, nt, nn, rts, rns, gsT, gsN, cT, cN);
+                nsite = 1;
+            }
+        }
+        if (end && nsite == 0u) break;
+    }
+}
+
+/* --------------------------------------------------------------------------
  * Synthetic generator (device twin of ss_synth.c; same ss_synth_core.h code).
  * ------------------------------------------------------------------------ */
 __global__ void ss_synth_depth_kernel(ss_synth_k_t k, uint64_t first, uint64_t n, uint8_t *ref,
@@ -2380,8 +2795,8 @@ int ss_launch_tab_fingerprint(const uint8_t *tab, unsigned long long *out3, hipS
     return (int)hipGetLastError();
 }
 
-int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, hipStream_t s,
-                    const hipEvent_t *ev)
+int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, int wild_grid,
+                    hipStream_t s, const hipEvent_t *ev)
 {
     hipError_t e;
     if (ev) (void)hipEventRecord(ev[0], s);
@@ -2392,6 +2807,8 @@ int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int de
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[2], s);
     hipLaunchKernelGGL(ss_score_deep, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(ss_score_wild, dim3(wild_grid), dim3(SS_WILD_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[3], s);
     return (int)hipSuccess;

@@ -46,6 +46,9 @@ def test_bench_json_contract():
         assert v["insts_per_site"] > 50 and 0 < v["issue_frac_lower_bound"] < 1.0, v
         # the clock from the profiled pass's own cycles and durations (never above MI355X's 2.4 GHz)
         assert 0.5 < v["clock_ghz_profiled"] <= 2.45 and v["kernel_ms_profiled"] > 0, v
+        # the rocprofv3 kernel trace of the same launches beside the HIP-event mean
+        kt = rf["kernel_ms_rocprof_trace"]
+        assert kt["dispatches"] > 0 and kt["warm_dispatches_ms"] > 0 and kt["hip_events_ms"] == rf["avg_kernel_ms"]
     cb = r["cpu_baseline"]
     assert cb["cores"] == 1 and cb["value"] > 0 and cb["parity_vs_gpu"] is True
     hf = r["host_fed"]                      # PCIe-inclusive ss_score_batch_host, never `value`
