@@ -99,6 +99,9 @@ struct ss_score_args {
 #ifndef SS_WIDE_BLOCK
 #define SS_WIDE_BLOCK      768   /* 12 waves, one workgroup per CU (168 VGPRs: 3 waves per SIMD) */
 #endif
+#ifndef SS_ROUTE_DEEP
+#define SS_ROUTE_DEEP      1024  /* a sample past this many reads: the deep kernel, not the group kernel */
+#endif
 #ifndef SS_WIDE_MAXSLOTS
 #define SS_WIDE_MAXSLOTS   2048  /* reads per sample the group kernel sorts (A/B builds may lower it) */
 #endif

@@ -1426,11 +1426,28 @@ __device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, boo
         wave_sync();                                     /* the pass's records are read */
     }
     ok = ok && !wild;
-    /* sites the lane path does not score: the group kernel's list (one
-     * segment per wave, no atomics) */
-    const uint64_t out = __ballot(insite && !ok);
+    /* sites with a sample past SS_ROUTE_DEEP reads go straight to the deep
+     * kernel's list (one atomic per wave), where its counting sort beats the
+     * group kernel's network */
+    const bool todeep = insite && !ok && formed && (nt > SS_ROUTE_DEEP || nn > SS_ROUTE_DEEP);
+    const uint64_t dm = __ballot(todeep);
+    if (dm) {
+        const ss_score_args &k = kernarg_args();
+        uint32_t d0 = 0;
+        if (lane == (uint32_t)__builtin_ctzll(dm)) d0 = atomicAdd(k.deep2_count, (uint32_t)__popcll(dm));
+        d0 = (uint32_t)__builtin_amdgcn_readlane((int)d0, (int)__builtin_ctzll(dm));
+        if (todeep) {
+            const uint32_t d = d0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
+            if (d < k.deep_cap) k.deep2_list[d] = s;
+            else atomicOr(k.err, SS_KERR_DEEP_OVERFLOW);
+        }
+    }
+    /* the other sites the lane path does not score: the group kernel's list
+     * (one segment per wave, no atomics) */
+    const bool listed = insite && !ok && !todeep;
+    const uint64_t out = __ballot(listed);
     if (out) {
-        if (insite && !ok) {
+        if (listed) {
             const uint32_t d = ndeep + __builtin_amdgcn_mbcnt_hi((uint32_t)(out >> 32),
                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)out, 0u));
             const ss_score_args &k = kernarg_args();
@@ -2325,26 +2342,28 @@ namespace {
 
 #define BN_WAVES (SS_DEEP_BLOCK / 64)
 #define BN_SLOTS 640                    /* bin slots per sample: group A 256, C / G / T 128 each */
-#define BN_WORDS (BN_SLOTS / 2)         /* 16-bit counts, two per word */
 #define BN_ROWS (BN_SLOTS / 64)         /* compaction rows: A 0..3, C 4..5, G 6..7, T 8..9 */
 #define BN_SITES 32                     /* sites per fold round: lane = (site, sample) */
 #define BN_CHUNK 16                     /* list entries a wave draws at a time */
-#define BN_ENT_CAP 6384                 /* runs per wave: a whole site always fits an empty list */
+#define BN_ENT_CAP 6072                 /* runs per wave: a whole site always fits an empty list */
 #define BN_FK_ZERO 256
 static_assert(BN_ENT_CAP >= 2 * (BN_SLOTS + SS_BINS_MAXN / 511 + 1), "a site's runs fit an empty list");
 
 struct alignas(16) BinsLds {
-    uint32_t hist[2][BN_WORDS];          /* tumor, normal: slot s = 16-bit half s & 1 of word s >> 1 */
-    uint2    slut[2][32];                /* per sample, read nt16 | strand << 4: histogram byte offset << 8 |
-                                            log2(bytes per minq), and the count's half (1 << 16 strand) */
-    uint16_t ent[BN_ENT_CAP];            /* runs: q | strand << 6 | count << 7 */
+    uint32_t hist[2][BN_SLOTS];          /* tumor, normal: one 32-bit count per slot (both strands of a
+                                            minq in different words: fewer lanes on one LDS address) */
+    uint32_t slut[32];                   /* read nt16 | strand << 4: histogram byte offset of its minq-0 slot
+                                            << 8 | log2(bytes per minq) */
+    union {
+        uint16_t ent[BN_ENT_CAP];        /* runs: q | strand << 6 | count << 7 */
+        SlotRes  res[2 * BN_SITES];      /* after a round's fold: its results, for the decision */
+    };
     uint16_t u_gs[2 * BN_SITES][6];      /* unit: first run of groups 0..3, then the unit's end */
     uint32_t u_cnt[2 * BN_SITES][4];     /* unit: contributing reads per group */
     uint32_t u_rms[2 * BN_SITES];        /* unit: rms sum (< 2^16 reads x 3600) */
     uint32_t u_n[2 * BN_SITES];          /* unit: non-deleted depth */
     uint32_t s_site[BN_SITES];
     uint32_t s_refc[BN_SITES];           /* ref char | nt16 << 8 */
-    SlotRes  res[2 * BN_SITES];
 };
 
 /* Histogram slots of one sample.  A read of minq < 64 whose clamped q is > 0
@@ -2359,20 +2378,20 @@ struct alignas(16) BinsLds {
  * sends its site to ss_score_wild (never produced by short-read aligners). */
 __device__ __forceinline__ uint32_t bn_gbase(uint32_t g) { return g ? 128u * (g + 1u) : 0u; }
 
-/* the per-sample lookup rows for a site of reference code ref16: lane =
- * sample << 5 | strand << 4 | read nt16 (bam_nt16_nt4_table semantics,
- * :153-154: '=' is the reference, N / IUPAC count as A without hasbase) */
+/* the lookup rows for a site of reference code ref16: lane = strand << 4 |
+ * read nt16 (bam_nt16_nt4_table semantics, :153-154: '=' is the reference,
+ * N / IUPAC count as A without hasbase) */
 __device__ __forceinline__ void bn_slut_build(BinsLds &B, uint32_t ref16)
 {
     const uint32_t lane = lane_id();
-    const uint32_t smp = lane >> 5, st = (lane >> 4) & 1u, nt16 = lane & 15u;
+    const uint32_t st = (lane >> 4) & 1u, nt16 = lane & 15u;
     const uint32_t code = nt16 ? nt16 : ref16;
     const uint32_t nt4 = code == 1u ? 0u : code == 2u ? 1u : code == 4u ? 2u : code == 8u ? 3u : 4u;
     const uint32_t hb = nt4 < 4u ? 1u : 0u, base = hb ? nt4 : 0u;
-    /* byte offset of minq 0's word in the sample's histogram: A 4 hasbase,
-     * else 2 gb; bytes per minq: A 8, else 4 */
-    const uint32_t wb = base ? 2u * bn_gbase(base) : 4u * hb;
-    B.slut[smp][lane & 31u] = make_uint2(wb << 8 | (base ? 2u : 3u), 1u << (16u * st));
+    /* byte offset of the read's minq-0 slot: A 4 (2 hasbase + strand), else
+     * 4 (gb + strand); bytes per minq: A 16, else 8 */
+    const uint32_t wb = base ? 4u * (bn_gbase(base) + st) : 4u * (2u * hb + st);
+    if (lane < 32u) B.slut[lane] = wb << 8 | (base ? 3u : 4u);
 }
 
 /* run code (q | strand << 6) of a slot of group g: q = max(minq, 4) */
@@ -2382,45 +2401,75 @@ __device__ __forceinline__ uint32_t bn_code(uint32_t slot, uint32_t g)
     return max(minq, 4u) | (slot & 1u) << 6;
 }
 
-/* one sample's reads into its (zeroed) histogram, eight loads in flight per
- * lane (their index clamped to the last read, so no load is predicated);
- * adds the rms terms (:173-174) to rs; true when a read needs ss_score_wild */
-__device__ __forceinline__ bool bn_pass(const uint32_t *reads, uint32_t n, const uint2 *slut, uint32_t cap,
-                                        uint32_t *hist, uint32_t &rs)
+/* eight reads per lane from reads[i0 ..] (lane + 64 j), indices clamped to
+ * the last read so no load is predicated; none for an empty sample */
+__device__ __forceinline__ void bn_issue(const uint32_t *reads, uint32_t n, uint32_t i0, uint32_t (&rd)[8])
 {
     const uint32_t lane = lane_id();
-    bool wild = false;
-    char *hb = reinterpret_cast<char *>(hist);
-    for (uint32_t i0 = 0; i0 < n; i0 += 8u * 64u) {
-        uint32_t rd[8];
+    if (n) {                                          /* wave-uniform */
 #pragma unroll
         for (uint32_t j = 0; j < 8u; ++j) rd[j] = __builtin_nontemporal_load(reads + min(i0 + lane + j * 64u, n - 1u));
-        /* the eight lookups first, then the addresses (pinned in registers:
-         * the compiler would otherwise sink each lookup into its atomic's
-         * branch and wait for it there), then the atomics */
-        uint32_t x[8], addr[8], val[8];
+    } else {
 #pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) {
-            x[j] = i0 + lane + j * 64u < n ? rd[j] : 0u;      /* 0: no contribution, no rms */
-            const uint2 e = slut[(x[j] >> 16) & 31u];
-            addr[j] = e.x;
-            val[j] = e.y;
-        }
+        for (uint32_t j = 0; j < 8u; ++j) rd[j] = 0u;
+    }
+}
+
+/* eight reads of one sample (rd[j] = read i0 + lane + 64 j) into its histogram */
+__device__ __forceinline__ void bn_count8(const uint32_t (&rd)[8], uint32_t i0, uint32_t n, const uint32_t *slut,
+                                          uint32_t cap, char *hb, uint32_t &rs, bool &wild)
+{
+    const uint32_t lane = lane_id();
+    /* the eight lookups first, then the addresses (pinned in registers: the
+     * compiler would otherwise sink each lookup into its atomic's branch and
+     * wait for it there), then the atomics */
+    uint32_t x[8], addr[8];
 #pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) {
-            const uint32_t minq = min(x[j] & 0xffu, (x[j] >> 8) & 0xffu);
-            addr[j] = (addr[j] >> 8) + (minq << (addr[j] & 31u));
-            asm volatile("" : "+v"(addr[j]), "+v"(val[j]));
-        }
+    for (uint32_t j = 0; j < 8u; ++j) {
+        x[j] = i0 + lane + j * 64u < n ? rd[j] : 0u;          /* 0: no contribution, no rms */
+        addr[j] = slut[(x[j] >> 16) & 31u];
+    }
 #pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) {
-            const uint32_t bq = (x[j] >> 8) & 0xffu;
-            const uint32_t minq = min(x[j] & 0xffu, bq);
-            const uint32_t t = min(x[j] & 0x7fu, cap);
-            rs += t * t;
-            const bool w = minq >= 64u || (minq < 4u && bq >= 64u);
-            wild |= w;
-            if (bq != 0u && !w) atomicAdd(reinterpret_cast<uint32_t *>(hb + addr[j]), val[j]);
+    for (uint32_t j = 0; j < 8u; ++j) {
+        const uint32_t minq = min(x[j] & 0xffu, (x[j] >> 8) & 0xffu);
+        addr[j] = (addr[j] >> 8) + (minq << (addr[j] & 31u));
+        asm volatile("" : "+v"(addr[j]));
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j) {
+        const uint32_t bq = (x[j] >> 8) & 0xffu;
+        const uint32_t minq = min(x[j] & 0xffu, bq);
+        const uint32_t t = min(x[j] & 0x7fu, cap);
+        rs += t * t;
+        const bool w = minq >= 64u || (minq < 4u && bq >= 64u);
+        wild |= w;
+        if (bq != 0u && !w) atomicAdd(reinterpret_cast<uint32_t *>(hb + addr[j]), 1u);
+    }
+}
+
+/* one sample's reads into its (zeroed) histogram: the first 512 arrive in
+ * `pre` (issued one site ahead and used in place: a register copy of loads
+ * in flight would wait for every younger load, the next site's among them),
+ * the rest 512 at a time, double-buffered; adds the rms terms (:173-174) to rs; true when a
+ * read needs ss_score_wild */
+__device__ __forceinline__ bool bn_pass(const uint32_t *reads, uint32_t n, const uint32_t (&pre)[8],
+                                        const uint32_t *slut, uint32_t cap, uint32_t *hist, uint32_t &rs)
+{
+    bool wild = false;
+    char *hb = reinterpret_cast<char *>(hist);
+    if (n) bn_count8(pre, 0u, n, slut, cap, hb, rs, wild);
+    if (n > 8u * 64u) {                               /* deep samples: each batch issued before the one before it is counted */
+        uint32_t rd[8];
+        bn_issue(reads, n, 8u * 64u, rd);
+        for (uint32_t i0 = 8u * 64u; i0 < n; i0 += 8u * 64u) {
+            uint32_t nx[8];
+            const bool more = i0 + 8u * 64u < n;
+            if (more) bn_issue(reads, n, i0 + 8u * 64u, nx);
+            bn_count8(rd, i0, n, slut, cap, hb, rs, wild);
+            if (more) {
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j) rd[j] = nx[j];
+            }
         }
     }
     return wild;
@@ -2436,7 +2485,6 @@ __device__ __forceinline__ uint32_t bn_runs(const uint32_t *hist, uint16_t *ent,
                                             uint32_t (&cnt)[4])
 {
     const uint32_t lane = lane_id();
-    const uint16_t *h16 = reinterpret_cast<const uint16_t *>(hist);
     uint32_t part = 0;
 #pragma unroll
     for (uint32_t r = 0; r < BN_ROWS; ++r) {
@@ -2445,7 +2493,7 @@ __device__ __forceinline__ uint32_t bn_runs(const uint32_t *hist, uint16_t *ent,
         const uint32_t gb = bn_gbase(g), gsz = g ? 128u : 256u;
         if (r == r0) gs[g] = pos;
         const uint32_t slot = gb + gsz - 1u - (64u * (r - r0) + lane);
-        const uint32_t c = h16[slot];
+        const uint32_t c = hist[slot];
         const uint32_t code = bn_code(slot, g);
         if (!__ballot(c > 511u)) {
             const uint64_t m = __ballot(c != 0u);
@@ -2608,6 +2656,46 @@ __device__ __forceinline__ void bn_unit_info(BinsLds &B, uint32_t i, uint32_t s,
     wave_sync();
 }
 
+/* descriptors of a chunk of the wave's list, lane i < BN_CHUNK = entry i */
+struct BnDesc {
+    uint32_t s, ot, on, nt, nn;
+    uint32_t fl;                             /* usable (well formed, <= SS_BINS_MAXN per sample) | ref << 8 | nt16 << 16 */
+};
+
+/* lane i's copy of a descriptor, wave-uniform */
+__device__ __forceinline__ uint32_t bn_rl(uint32_t v, uint32_t i)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i);
+}
+
+/* draw the next chunk of the list from the kernel's counter and load its
+ * descriptors into lanes 0 .. BN_CHUNK - 1 (not waited for); returns its
+ * entries, 0 at the end of the list */
+__device__ __forceinline__ uint32_t bn_grab_desc(uint32_t count, BnDesc &d)
+{
+    const uint32_t lane = lane_id();
+    const ss_score_args &k = kernarg_args();
+    uint32_t ch = 0;
+    if (lane == 0u) ch = atomicAdd(k.deep_next, 1u);
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * BN_CHUNK;
+    if (c0 >= count) return 0u;
+    const uint32_t len = min(count - c0, (uint32_t)BN_CHUNK);
+    const uint32_t end_t = k.off_t[k.n_sites], end_n = k.off_n[k.n_sites];
+    const uint32_t e = c0 + min(lane, len - 1u);
+    const uint32_t st = k.deep2_list[e];
+    const uint32_t ot = k.off_t[st], ot1 = k.off_t[st + 1], on = k.off_n[st], on1 = k.off_n[st + 1];
+    const uint32_t rc = k.ref[st];
+    const bool ok = site_wellformed(ot, ot1, end_t) && site_wellformed(on, on1, end_n) && ot1 - ot <= SS_BINS_MAXN &&
+                    on1 - on <= SS_BINS_MAXN;
+    d.s = st;
+    d.ot = ot;
+    d.on = on;
+    d.nt = ok ? ot1 - ot : 0u;
+    d.nn = ok ? on1 - on : 0u;
+    d.fl = (ok ? 1u : 0u) | rc << 8 | (uint32_t)ss_tab_nt16(k.m)[rc] << 16;
+    return len;
+}
+
 /* hand a site on to ss_score_wild */
 __device__ __forceinline__ void bn_to_wild(uint32_t s)
 {
@@ -2635,57 +2723,82 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     BinsLds &B = BL[wv];
     const uint32_t lane = lane_id();
-    uint32_t cur = 0, cend = 0;                     /* the wave's current list entries (uniform) */
+    const uint32_t cap = (uint32_t)a.m.cap_mapQ;
+    /* Descriptors of a chunk of BN_CHUNK list entries sit in lanes 0..15 (one
+     * entry per lane, read out with readlane), the next chunk's are loaded
+     * while this one is scored, and the next site's first reads while the
+     * site before it is counted: no dependent load chain per site. */
+    BnDesc D, ND;
+    uint32_t clen = bn_grab_desc(count, D);         /* entries of the current chunk (uniform) */
+    uint32_t nlen = clen ? bn_grab_desc(count, ND) : 0u;
+    uint32_t idx = 0;                               /* the next entry of the current chunk */
     uint32_t nsite = 0, nent = 0;                   /* the current round */
-    bool end = false;
     /* the site whose histograms are built (s, depths, reference, rms sums) */
     uint32_t s = 0, nt = 0, nn = 0, refc = 0, ref16 = 0;
     uint32_t rts = 0, rns = 0;
-    /* one bn_round call site: each iteration fetches and counts a site, writes
-     * its runs when they fit the round, and folds the round when it is full,
-     * when the site's runs did not fit (they are written again behind the
-     * folded round: the histograms stay), or at the end of the list */
+    /* the first 512 reads per sample of the next site */
+    uint32_t pft[8], pfn[8];
+    if (clen) {
+        const ss_score_args &k = kernarg_args();
+        bn_issue(k.reads_t + bn_rl(D.ot, 0u), bn_rl(D.nt, 0u), 0u, pft);
+        bn_issue(k.reads_n + bn_rl(D.on, 0u), bn_rl(D.nn, 0u), 0u, pfn);
+    }
+    /* one bn_round call site: each iteration counts a site, writes its runs
+     * when they fit the round, and folds the round when it is full, when the
+     * site's runs did not fit (they are written again behind the folded
+     * round: the histograms stay), or at the end of the list */
     for (;;) {
         bool ready = false;
-        if (!end && cur == cend) {
-            uint32_t ch = 0;
-            if (lane == 0u) ch = atomicAdd(kernarg_args().deep_next, 1u);
-            cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * BN_CHUNK;
-            end = cur >= count;
-            cend = end ? cur : min(cur + BN_CHUNK, count);
+        if (clen && idx == clen) {                  /* the next chunk becomes the current one */
+            D = ND;
+            clen = nlen;
+            idx = 0;
+            nlen = clen ? bn_grab_desc(count, ND) : 0u;
         }
+        const bool end = clen == 0u;
         if (!end) {
             const ss_score_args &k = kernarg_args();
-            s = k.deep2_list[cur++];
-            const uint32_t ot = k.off_t[s], ot1 = k.off_t[s + 1], on = k.off_n[s], on1 = k.off_n[s + 1];
-            const uint32_t end_t = k.off_t[k.n_sites], end_n = k.off_n[k.n_sites];
-            if (!site_wellformed(ot, ot1, end_t) || !site_wellformed(on, on1, end_n) || ot1 - ot > SS_BINS_MAXN ||
-                on1 - on > SS_BINS_MAXN) {
+            s = bn_rl(D.s, idx);
+            const uint32_t ot = bn_rl(D.ot, idx), on = bn_rl(D.on, idx);
+            nt = bn_rl(D.nt, idx);
+            nn = bn_rl(D.nn, idx);
+            const uint32_t fl = bn_rl(D.fl, idx);
+            ++idx;
+            uint32_t pt[8], pn[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8u; ++j) { pt[j] = pft[j]; pn[j] = pfn[j]; }
+            /* the next site's first reads go out now: the chunk's next entry,
+             * or the next chunk's first */
+            if (idx < clen) {
+                bn_issue(k.reads_t + bn_rl(D.ot, idx), bn_rl(D.nt, idx), 0u, pft);
+                bn_issue(k.reads_n + bn_rl(D.on, idx), bn_rl(D.nn, idx), 0u, pfn);
+            } else if (nlen) {
+                bn_issue(k.reads_t + bn_rl(ND.ot, 0u), bn_rl(ND.nt, 0u), 0u, pft);
+                bn_issue(k.reads_n + bn_rl(ND.on, 0u), bn_rl(ND.nn, 0u), 0u, pfn);
+            }
+            if (!(fl & 1u)) {
                 bn_to_wild(s);                         /* it reports malformed offsets (-2) */
-                continue;
+            } else {
+                refc = (fl >> 8) & 0xffu;
+                ref16 = fl >> 16;
+                bn_slut_build(B, ref16);
+                {
+                    uint4 *h4 = reinterpret_cast<uint4 *>(&B.hist[0][0]);
+                    for (uint32_t i = lane; i < BN_SLOTS / 2u; i += 64u) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+                }
+                wave_sync();
+                uint32_t rt = 0, rn = 0;
+                bool wild = bn_pass(k.reads_t + ot, nt, pt, B.slut, cap, B.hist[0], rt);
+                wild |= bn_pass(k.reads_n + on, nn, pn, B.slut, cap, B.hist[1], rn);
+                if (__ballot(wild)) {                  /* ss_score_wild's windows and baseQ bins */
+                    bn_to_wild(s);
+                } else {
+                    rts = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(rt), 63);   /* rms sums */
+                    rns = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(rn), 63);
+                    wave_sync();
+                    ready = true;
+                }
             }
-            nt = ot1 - ot;
-            nn = on1 - on;
-            refc = k.ref[s];
-            ref16 = ss_tab_nt16(k.m)[refc];
-            bn_slut_build(B, ref16);
-            {
-                uint4 *h4 = reinterpret_cast<uint4 *>(&B.hist[0][0]);
-                for (uint32_t i = lane; i < BN_WORDS / 2u; i += 64u) h4[i] = make_uint4(0u, 0u, 0u, 0u);
-            }
-            wave_sync();
-            const uint32_t cap = (uint32_t)k.m.cap_mapQ;
-            uint32_t rt = 0, rn = 0;
-            bool wild = bn_pass(k.reads_t + ot, nt, B.slut[0], cap, B.hist[0], rt);
-            wild |= bn_pass(k.reads_n + on, nn, B.slut[1], cap, B.hist[1], rn);
-            if (__ballot(wild)) {                      /* ss_score_wild's windows and baseQ bins */
-                bn_to_wild(s);
-                continue;
-            }
-            rts = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(rt), 63);   /* rms sums over the wave */
-            rns = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(rn), 63);
-            wave_sync();
-            ready = true;
         }
         uint32_t gsT[5], gsN[5], cT[4], cN[4];
         if (ready && nsite < BN_SITES) {
