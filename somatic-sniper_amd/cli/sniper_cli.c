@@ -9,7 +9,7 @@
  *   pileup thread                      scorer threads (one per GPU)
  *   ----------------------------       -------------------------------------
  *   pack sites into batch k      ->    ss_score_batch_host(batch k) on the
- *   (while earlier batches are         thread's own context / device, then,
+ *   (while earlier batches are         slot's context / device, then,
  *   being scored)                      in batch order, dqstats + writer for
  *                                      every emitted site ((tid, pos) order)
  *
@@ -24,7 +24,9 @@
  * need one, so this is optional), the contigs are cut into SS_CONTIG_GROUPS
  * (default 4) ranges of about equal compressed size, and each range runs its
  * own pileup (both files read from the range's first records, bam_index.h),
- * batches and scorers; the ranges' outputs are concatenated in contig order.
+ * batches and scorer threads; scorer k of every range shares the process's
+ * context k (one per device, created once: shared_ctx), and the ranges'
+ * outputs are concatenated in contig order.
  * Each walk's state at a range start is seeded from the last record its file
  * loads before the range (column_pileup.h), so the sites, entries and output
  * bytes are those of the single streaming walk.
@@ -138,16 +140,38 @@ typedef struct {
     pthread_cond_t cv;
     FILE *dump;
     int pileup_only;
-    /* GPU scorers, created on their threads while the pileup runs */
+    /* GPU scorers: scorer slot k uses the process's context k (shared_ctx) */
     ss_params_t prm;
     int n_dev, device[MAX_DEV];
-    ss_ctx_t *ctx[MAX_DEV];
 } run_t;
 
 typedef struct {
     run_t *R;
     int k;                    /* scorer index */
 } scorer_arg_t;
+
+/* One GPU context per scorer slot for the whole process: the streaming walk's
+ * scorer k and scorer k of every contig range share it, one batch at a time
+ * (a context takes one launch at a time, include/sniper_amd.h), so a range
+ * costs no context creation (table upload and fingerprint, about 0.25 s each
+ * in round 5).  Created by the first scorer thread that needs it, while the
+ * pileup runs. */
+static ss_ctx_t *g_ctx[MAX_DEV];
+static int g_ctx_rc[MAX_DEV];
+static pthread_mutex_t g_ctx_make_mu[MAX_DEV], g_ctx_use_mu[MAX_DEV];
+
+static ss_ctx_t *shared_ctx(const ss_params_t *prm, int k, int device)
+{
+    pthread_mutex_lock(&g_ctx_make_mu[k]);
+    if (!g_ctx[k] && !g_ctx_rc[k]) g_ctx_rc[k] = ss_ctx_create(prm, device, &g_ctx[k]);
+    const int rc = g_ctx_rc[k];
+    pthread_mutex_unlock(&g_ctx_make_mu[k]);
+    if (rc) {
+        fprintf(stderr, "[bam-somaticsniper] cannot create the GPU scorer: %s\n", ss_strerror(rc));
+        exit(1);
+    }
+    return g_ctx[k];
+}
 
 static int failed_get(run_t *R) { return __atomic_load_n(&R->failed, __ATOMIC_ACQUIRE); }
 static void failed_set(run_t *R) { __atomic_store_n(&R->failed, 1, __ATOMIC_RELEASE); }
@@ -232,13 +256,8 @@ static void *scorer_main(void *arg)
     ss_ctx_t *ctx = NULL;
     if (!R->pileup_only) {
         /* host tables (shared by the process) + device upload overlap the BAM decode and pileup */
-        const int rc = ss_ctx_create(&R->prm, R->device[k], &ctx);
+        ctx = shared_ctx(&R->prm, k, R->device[k]);
         stamp("scorer ready");
-        if (rc) {
-            fprintf(stderr, "[bam-somaticsniper] cannot create the GPU scorer: %s\n", ss_strerror(rc));
-            exit(1);
-        }
-        R->ctx[k] = ctx;
     }
     pthread_mutex_lock(&R->mu);
     for (;;) {
@@ -247,7 +266,12 @@ static void *scorer_main(void *arg)
         const uint64_t s = R->seq_claim++;
         batch_t *b = &R->bat[s % (uint64_t)R->n_bat];
         pthread_mutex_unlock(&R->mu);
-        const long ncalls = failed_get(R) ? -1 : score_batch(R, ctx, b);
+        long ncalls = -1;
+        if (!failed_get(R)) {
+            pthread_mutex_lock(&g_ctx_use_mu[k]);      /* the context is shared with other ranges' scorer k */
+            ncalls = score_batch(R, ctx, b);
+            pthread_mutex_unlock(&g_ctx_use_mu[k]);
+        }
         stamp("batch scored");
         if (debug_batches)                                  /* SS_DEBUG_BATCHES=1: one line per scored batch */
             fprintf(stderr, "[batch] run %p scorer %d seq %llu sites %zu first %u:%u calls %ld\n", (void *)R, k,
@@ -461,9 +485,8 @@ static void *group_main(void *arg)
         if (f2) bgzf_close(f2);
     }
     run_scorers_finish(R);
-    /* release the range's GPU contexts and batches here, while other ranges still run */
-    for (int k = 0; k < R->n_dev; ++k)
-        if (R->ctx[k]) { ss_ctx_destroy(R->ctx[k]); R->ctx[k] = NULL; }
+    /* release the range's batches here, while other ranges still run (the
+     * GPU contexts are the process's, destroyed at exit) */
     for (int k = 0; k < R->n_bat; ++k) batch_free(&R->bat[k]);
     R->n_bat = 0;
     return NULL;
@@ -603,6 +626,10 @@ static int run_groups(run_t *base, const char *bam1, const char *bam2, int mapq,
 int main(int argc, char *argv[])
 {
     t_start = now_s();
+    for (int k = 0; k < MAX_DEV; ++k) {
+        pthread_mutex_init(&g_ctx_make_mu[k], NULL);
+        pthread_mutex_init(&g_ctx_use_mu[k], NULL);
+    }
     timing = getenv("SS_TIMING") != NULL;
     debug_batches = getenv("SS_DEBUG_BATCHES") != NULL;
     ss_params_t prm;
@@ -709,7 +736,7 @@ int main(int argc, char *argv[])
     for (int k = 0; k < R.n_bat; ++k) batch_free(&R.bat[k]);
     stamp("output written");
     for (int k = 0; k < R.n_dev; ++k)
-        if (R.ctx[k]) ss_ctx_destroy(R.ctx[k]);
+        if (g_ctx[k]) ss_ctx_destroy(g_ctx[k]);
     if (R.dump) fclose(R.dump);
     fclose(R.out);
     stamp("exit");
