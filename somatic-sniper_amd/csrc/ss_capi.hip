@@ -26,6 +26,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -52,6 +53,7 @@ struct ss_ctx {
     uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6..7] listed
                                  entries | segments << 32, [8] the group kernel's chunk counter,
                                  [9] the deep kernel's chunk counter, [10] deep3 count,
+                                 [12..15] the device generator's read totals (2 x u64),
                                  [16..21] the table fingerprint (3 x u64) */
     uint32_t *d_deep_list;
     uint32_t deep_cap;
@@ -76,7 +78,8 @@ struct ss_ctx {
     /* device memory (dev_alloc): blocks in use, blocks outgrown but possibly still read */
     std::vector<dev_blk> *blocks, *retired;
     uint64_t fp_expect[3];    /* host fingerprint of the uploaded tables: coef, lhet, the rest */
-    uint8_t fast_thr[256];    /* SS_TAB_FAST (fast_table) */
+    float near_esr[132];      /* SS_TAB_ESR (near_tables) */
+    float near_cmin[132];     /* SS_TAB_CMIN */
     int fast_ok;              /* SS_MF_FAST */
     int counted;              /* included in g_live */
 };
@@ -275,42 +278,60 @@ static void ctx_quiesce(ss_ctx_t *c)
     if (c->hstream) hipStreamSynchronize(c->hstream);
 }
 
-/* The main kernel's early exit (ss_kernels.hip ln_classify): for n = 1 .. 128
- * reads per sample, the smallest count c24 of reads with minq >= 24 such that
- *   24 * (m[0] + .. + m[c24 - 1]) * (1 - 1e-4) + min coef[q][n'][n'] >= 1,
- *   m[k] = min(fk[0 .. k]),
- * over q in [4, 63] and n' in [1, n] (sniper_maqcns.c:184-196: the non-reference
- * homozygotes' p when every read is on the reference); 255 = never.  The k-th
- * q >= 24 read of the walk weighs fk[w] with w <= k (w counts per strand), so
- * its weight is >= m[k] whatever the shape of fk: fk[n] = theta^n (1 - eta) +
- * eta (sniper_maqcns.c:72) decreases for theta < 1 but increases for the
- * theta > 1 that -T accepts (main.c:83 has no range check), and then m[k] =
- * fk[0].  The 1e-4 margin covers the float accumulation of esum (<= 128
- * roundings of 2^-24 relative each).  Enabled only with q_r >= 1, so a
- * heterozygote never ties the reference homozygote in sniper_glf2cns. */
-static int fast_table(const ss_host_model_t &hm, uint8_t thr[256])
+/* float(x) rounded towards -inf */
+static float round_down_f(double x)
 {
-    memset(thr, 255, 256);
+    float f = (float)x;
+    if ((double)f > x) f = nextafterf(f, -INFINITY);
+    return f;
+}
+
+/* The bounds of the main kernel's early exit (ss_kernels.hip ln_classify,
+ * DESIGN.md 4.1): for a sample whose reference-base group has c of its
+ * contributing reads at minq >= 24, and tot contributing reads in all,
+ *   esr[c]    <= esum[ref]:  24 (m[0] + .. + m[c - 1]) (1 - 1e-4), m[k] = min(fk[0 .. k]);
+ *   cmin[tot] <= lh + coef[q][tot][k] over q in [4, 63], k in [1, tot] and
+ *                lh = -4.343 lhet[..] (min with 0), less 0.01,
+ * so every genotype without the reference base has p >= esr[c] + cmin[tot]
+ * (its e sums esum[ref] and other non-negative esums, sniper_maqcns.c:184-210).
+ * The k-th q >= 24 read of the reference group's walk weighs fk[w] with w <= k
+ * (w counts per strand), so its weight is >= m[k] whatever the shape of fk:
+ * fk[n] = theta^n (1 - eta) + eta (sniper_maqcns.c:72) decreases for theta < 1
+ * but increases for the theta > 1 that -T accepts (main.c:83 has no range
+ * check), and then m[k] = fk[0].  The 1e-4 margin covers the float
+ * accumulation of esum (<= 128 roundings of 2^-24 relative each), the 0.01
+ * the float rounding of p; both tables round down.  Enabled only with
+ * q_r >= 1 and finite tables. */
+static int near_tables(const ss_host_model_t &hm, float esr[132], float cmin[132])
+{
+    for (int i = 0; i < 132; ++i) {
+        esr[i] = 0.0f;
+        cmin[i] = -1e30f;
+    }
     if (hm.q_r_int < 1) return 0;
-    double F[130];
-    F[0] = 0.0;
-    double run_min = hm.fk[0];
-    for (int k = 0; k < 129; ++k) {
-        run_min = std::min(run_min, hm.fk[k < 255 ? k : 255]);
-        F[k + 1] = F[k] + run_min;
+    double F = 0.0, run_min = hm.fk[0];
+    for (int k = 0; k < 128; ++k) {
+        run_min = std::min(run_min, hm.fk[k]);
+        F += run_min;
+        esr[k + 1] = round_down_f(24.0 * F * (1.0 - 1e-4));
     }
-    double cm = 1e300;
-    int any = 0;
+    double lh = 0.0;
+    for (int i = 0; i < 65536; ++i) {
+        const double v = -4.343 * hm.lhet[i];
+        if (!std::isfinite(v)) return 0;
+        lh = std::min(lh, v);
+    }
     for (int n = 1; n <= 128; ++n) {
-        for (int q = 4; q < 64; ++q) cm = std::min(cm, hm.coef[(size_t)q << 16 | (size_t)n << 8 | (size_t)n]);
-        for (int c = 1; c <= n; ++c)
-            if (24.0 * F[c] * (1.0 - 1e-4) + cm >= 1.0) {
-                thr[n] = (uint8_t)c;
-                any = 1;
-                break;
+        double cm = 1e300;
+        for (int q = 4; q < 64; ++q)
+            for (int k = 1; k <= n; ++k) {
+                const double v = hm.coef[(size_t)q << 16 | (size_t)n << 8 | (size_t)k];
+                if (!std::isfinite(v)) return 0;
+                cm = std::min(cm, v);
             }
+        cmin[n] = round_down_f(cm + lh - 0.01);
     }
-    return any;
+    return std::isfinite(F) ? 1 : 0;
 }
 
 /* queue the fingerprint of the context's device tables (ss_tab_fingerprint)
@@ -332,7 +353,7 @@ static int tables_compare(const ss_ctx_t *c, const unsigned long long fp[3])
     if (fp[0] == c->fp_expect[0] && fp[1] == c->fp_expect[1] && fp[2] == c->fp_expect[2]) return SS_OK;
     fprintf(stderr, "[sniper_amd] device %d: the context's device tables no longer match the host's (%s%s%s differ)\n",
             c->device, fp[0] != c->fp_expect[0] ? "coef " : "", fp[1] != c->fp_expect[1] ? "lhet " : "",
-            fp[2] != c->fp_expect[2] ? "fk/qAdd/prior/nt16/fast" : "");
+            fp[2] != c->fp_expect[2] ? "fk/qAdd/prior/nt16/bounds" : "");
     return SS_E_TABLES;
 }
 
@@ -416,7 +437,7 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
         return SS_E_HIP;
     }
     hipStream_t hs = c->hstream;
-    c->fast_ok = fast_table(c->hm, c->fast_thr);
+    c->fast_ok = near_tables(c->hm, c->near_esr, c->near_cmin);
 #define TRY(x) do { if ((rc = (x)) != SS_OK) { ss_ctx_destroy(c); return rc; } } while (0)
     TRY(dev_alloc(c, (void **)&c->d_tab, SS_TAB_BYTES, hs));
     {
@@ -428,7 +449,8 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
             {SS_TAB_PRIOR, c->hm.prior, 160 * sizeof(int32_t)},
             {SS_TAB_JPRIOR, c->hm.jprior, 1600 * sizeof(int32_t)},
             {SS_TAB_NT16, ss_nt16_table, 256},
-            {SS_TAB_FAST, c->fast_thr, 256},
+            {SS_TAB_ESR, c->near_esr, 132 * sizeof(float)},
+            {SS_TAB_CMIN, c->near_cmin, 132 * sizeof(float)},
         };
         for (auto &pt : parts)
             if (hipMemcpyAsync(c->d_tab + pt.off, pt.src, pt.n, hipMemcpyHostToDevice, hs) != hipSuccess) {
@@ -895,8 +917,19 @@ extern "C" int ss_synth_batch_device(ss_ctx_t *c, const ss_synth_t *s, uint64_t 
             c->depth_tmp_n = 2 * (n + 1);
         }
         uint32_t *dt = c->d_depth_tmp, *dn = c->d_depth_tmp + (n + 1);
+        /* the 64-bit read totals (counters 12..15): the offsets are 32-bit */
+        unsigned long long *dsum = reinterpret_cast<unsigned long long *>(c->d_counters + 12);
         HIPCHK(hipMemsetAsync(dt, 0, 2 * (n + 1) * 4, st));
-        if (ss_launch_synth_depth(k, first, n, ref, dt, dn, st)) return SS_E_HIP;
+        HIPCHK(hipMemsetAsync(dsum, 0, 2 * sizeof(unsigned long long), st));
+        if (ss_launch_synth_depth(k, first, n, ref, dt, dn, dsum, st)) return SS_E_HIP;
+        unsigned long long sums[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(sums, dsum, sizeof(sums), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (sums[0] > 0xffffffffull || sums[1] > 0xffffffffull) {
+            fprintf(stderr, "[sniper_amd] ss_synth_batch_device: %llu tumor / %llu normal reads do not fit the "
+                            "batch's 32-bit offsets; use fewer sites per batch\n", sums[0], sums[1]);
+            return SS_E_INVAL;
+        }
         size_t need = 0;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, dt, off_t, (int)(n + 1), st));
         if (need > c->scan_tmp_sz) {

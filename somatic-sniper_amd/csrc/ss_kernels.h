@@ -19,13 +19,14 @@
 #define SS_TAB_PRIOR  (SS_TAB_QADD + (size_t)1024 * 4)            /* i32 [16 * 10]   */
 #define SS_TAB_JPRIOR (SS_TAB_PRIOR + (size_t)160 * 4)            /* i32 [16*10*10]  */
 #define SS_TAB_NT16   (SS_TAB_JPRIOR + (size_t)1600 * 4)          /* u8  [256]       */
-#define SS_TAB_FAST   (SS_TAB_NT16 + (size_t)256)                 /* u8  [256]: the early exit's c24 per depth */
-#define SS_TAB_BYTES  (SS_TAB_FAST + (size_t)256)
+#define SS_TAB_ESR    (SS_TAB_NT16 + (size_t)256)                 /* f32 [132]: the early exit's esum bound per c24 */
+#define SS_TAB_CMIN   (SS_TAB_ESR + (size_t)132 * 4)              /* f32 [132]: its coef + lh bound per depth */
+#define SS_TAB_BYTES  (SS_TAB_CMIN + (size_t)132 * 4)
 
 #define SS_MF_JOINT 1u
 #define SS_MF_LOH   2u
 #define SS_MF_GOR   4u
-#define SS_MF_FAST  8u   /* SS_TAB_FAST is valid (q_r >= 1): the main kernel's early exit may run */
+#define SS_MF_FAST  8u   /* SS_TAB_ESR / SS_TAB_CMIN are valid (q_r >= 1): the main kernel's early exit may run */
 
 struct ss_dev_model {
     const uint8_t *tab;      /* SS_TAB_* layout */
@@ -47,7 +48,8 @@ SS_TAB_ACCESSOR(qadd, int32_t, SS_TAB_QADD)
 SS_TAB_ACCESSOR(prior, int32_t, SS_TAB_PRIOR)
 SS_TAB_ACCESSOR(jprior, int32_t, SS_TAB_JPRIOR)
 SS_TAB_ACCESSOR(nt16, uint8_t, SS_TAB_NT16)
-SS_TAB_ACCESSOR(fast, uint8_t, SS_TAB_FAST)
+SS_TAB_ACCESSOR(esr, float, SS_TAB_ESR)
+SS_TAB_ACCESSOR(cmin, float, SS_TAB_CMIN)
 #undef SS_TAB_ACCESSOR
 
 /* Per-launch arguments of the scoring kernels. */
@@ -116,7 +118,7 @@ int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int de
 /* out3 (zeroed by the caller): fingerprint sums of coef, lhet and the rest (ss_host.h) */
 int ss_launch_tab_fingerprint(const uint8_t *tab, unsigned long long *out3, hipStream_t s);
 int ss_launch_synth_depth(const ss_synth_k_t &k, uint64_t first, uint64_t n, uint8_t *ref,
-                          uint32_t *dt, uint32_t *dn, hipStream_t s);
+                          uint32_t *dt, uint32_t *dn, unsigned long long *sums /* [2], zeroed */, hipStream_t s);
 int ss_launch_synth_reads(const ss_synth_k_t &k, uint64_t first, uint64_t n,
                           const uint32_t *off_t, const uint32_t *off_n, uint32_t *rt,
                           uint32_t *rn, hipStream_t s);

@@ -815,7 +815,7 @@ namespace {
 #define LN_P 4                       /* chunk loads in flight ahead of the key build */
 #define LN_WAVES (SS_MAIN_BLOCK / 64)
 #ifndef SS_EARLY_MAX_READS
-#define SS_EARLY_MAX_READS 72u       /* blocks of at most this mean (tumor + normal) reads per site take the early exit */
+#define SS_EARLY_MAX_READS 256u      /* blocks of at most this mean (tumor + normal) reads per site take the early exit */
 #endif
 
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -898,8 +898,9 @@ __device__ __forceinline__ uint32_t ln_elem(const uint32_t (&v)[R], int e)
  * ref-dependent part of its 16-bit order key (sample << 15 | base << 13 |
  * hasbase << 4 | strand << 3; bam_nt16_nt4_table semantics,
  * sniper_maqcns.c:19,153-154: single-base codes give their base with hasbase,
- * '=' the reference's, any other code counts as A without hasbase) and .y the
- * read's group count increment (1 << 8 * base).  Entry 0 belongs to a
+ * '=' the reference's, any other code counts as A without hasbase; bit 31 set
+ * when that base is not the reference's, for the early exit) and .y the read's
+ * group count increment (1 << 8 * base).  Entry 0 belongs to a
  * non-contributing read (clamped q = 0, or a pad): key 0xffff, no count.  Row
  * (sample, ref16) starts at byte 256 * (1 + sample * 16 + ref16) and a read
  * indexes it by (nt16 | strand << 4) * 8 = (read >> 13) & 0xf8, XOR-swizzled
@@ -923,8 +924,12 @@ __device__ __forceinline__ void ln_lut_build(uint2 *lut)
         const uint32_t code = nt16 ? nt16 : ref16;
         const uint32_t nt4 = code == 1u ? 0u : code == 2u ? 1u : code == 4u ? 2u : code == 8u ? 3u : 4u;
         const uint32_t hb = nt4 < 4u ? 1u : 0u, base = hb ? nt4 : 0u;
+        /* bit 31: the read's group is not the reference base's (the early
+         * exit's count pass; the key build keeps the low 16 bits) */
+        const uint32_t rcode = ref16 == 1u ? 0u : ref16 == 2u ? 1u : ref16 == 4u ? 2u : ref16 == 8u ? 3u : 0u;
         lut[(rw << 5) | ((i ^ rw) & 31u)] = rw == 0u ? make_uint2(0xffffu, 0u)
-                          : make_uint2(smp << 15 | base << 13 | hb << 4 | st << 3, 1u << (8u * base));
+                          : make_uint2(smp << 15 | base << 13 | hb << 4 | st << 3 | (base != rcode ? 1u << 31 : 0u),
+                                       1u << (8u * base));
     }
 }
 
@@ -1031,7 +1036,7 @@ __device__ __forceinline__ void ln_chunk(const LaneIn &in, const uint2 *lut, uin
         const uint32_t key = ent[t].x | minq[t] << 5 | (y[t] & 6u) | ln_nz(lo6[t]);   /* < 2^16 */
         ccnt += ent[t].y;
         const uint32_t e = c4 + (uint32_t)t;
-        if (e < LN_R) v[e] = key;                                   /* high half 0: a pad, see below */
+        if (e < LN_R) v[e] = key & 0xffffu;                         /* high half 0: a pad, see below */
         else v[LN_N - 1 - e] |= (key ^ 0xffffu) << 16;
     }
     /* rms terms min(mapQ & 0x7f, cap)^2 two at a time: the mapQ bytes of two
@@ -1475,10 +1480,18 @@ __device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, boo
     wave_sync();
 }
 
-/* the early exit's count pass over chunk c (ln_classify): per-sample group
- * counts of every read (contributing or not) and the reads of minq >= 24 */
+/* the early exit's count pass over chunk c (ln_classify): per sample the
+ * contributing reads' group counts (8-bit fields, as the key build's) and its
+ * contributing reads of minq >= 24.  A chunk with a contributing read whose
+ * group is not the reference base's (the lookup table's bit 31) is kept for
+ * the near-reference test: its four words go to the lane's LDS slot nfl
+ * (capture[nfl][lane], at most SS_NEAR_SLOTS), their flags to bits 4 nfl of
+ * fl_all and its sample (sb) to bit nfl of smp_all. */
+#define SS_NEAR_SLOTS 6u
 __device__ __forceinline__ void ln_count_chunk(const LaneIn &in, const uint2 *lut, uint32_t c, const uint32_t (&x)[4],
-                                               uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24)
+                                               uint32_t nrm, uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24,
+                                               uint4 *capture, uint32_t lane, uint32_t &nfl, uint32_t &fl_all,
+                                               uint32_t &smp_all)
 {
     const bool fa = c < in.nca;
     const int lim = (int)(fa ? in.na : in.nab) - (int)(4u * c);
@@ -1486,30 +1499,43 @@ __device__ __forceinline__ void ln_count_chunk(const LaneIn &in, const uint2 *lu
     asm("v_med3_i32 %0, %1, 0, 4" : "=v"(vl) : "v"(lim));
     asm("v_bfm_b32 %0, %1, 0" : "=v"(valid) : "v"(vl));
     const uint32_t row = fa ? in.la : in.lb;
-    uint32_t cc = 0, q = 0;
+    uint32_t minq[4];
+    uint2 ent[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         uint32_t vm;
         asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(vm) : "v"(valid), "i"(t));
         const uint32_t rd = x[t] & vm;
-        /* every read counts, contributing or not; a masked element reads entry 0 (no count) */
-        const uint32_t off = (((rd >> 13) & 0xf8u) ^ row) & vm;
-        cc += reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lut) + off)[1];
-        uint32_t minq;
         asm("v_min_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_1"
-            : "=v"(minq) : "v"(rd));
-        q += minq >= 24u ? 1u : 0u;
+            : "=v"(minq[t]) : "v"(rd));
+        /* a non-contributing read (clamped q = 0) or a masked element reads entry 0: no count, no flag */
+        const uint32_t off = __umul24(((rd >> 13) & 0xf8u) ^ row, ln_nz(minq[t] | (rd & 0x3f00u)));
+        ent[t] = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(lut) + off);
+    }
+    uint32_t cc = 0, q = 0, fl = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        cc += ent[t].y;
+        q += minq[t] >= 24u ? 1u : 0u;             /* minq >= 24: contributing */
+        fl |= (ent[t].x >> 31) << t;
     }
     cnt_t += cc;
     cnt_a += fa ? cc : 0u;
     c24 += fa ? q : q << 16;
+    if (fl != 0u && nfl < SS_NEAR_SLOTS) {
+        capture[nfl * 64u + lane] = make_uint4(x[0], x[1], x[2], x[3]);
+        fl_all |= fl << (4u * nfl);
+        smp_all |= (nrm | (fa ? 0u : 1u)) << nfl;
+        ++nfl;
+    }
 }
 
 /* the count pass over a block's chunks: groups of LN_P chunk loads in flight,
  * as in ln_keys, the tail mode fixed per instantiation (TM, ln_load) */
 template <int TM>
-__device__ __forceinline__ void ln_count_pass(const LaneIn &in, const uint2 *lut, uint32_t nch, uint32_t &cnt_a,
-                                              uint32_t &cnt_t, uint32_t &c24)
+__device__ __forceinline__ void ln_count_pass(const LaneIn &in, const uint2 *lut, uint32_t nch, uint32_t nrm,
+                                              uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24, uint4 *capture,
+                                              uint32_t lane, uint32_t &nfl, uint32_t &fl_all, uint32_t &smp_all)
 {
     uint32_t buf[2][LN_P][4];
     if (nch > 0u) {
@@ -1524,33 +1550,158 @@ __device__ __forceinline__ void ln_count_pass(const LaneIn &in, const uint2 *lut
             for (int j = 0; j < LN_P; ++j) ln_load<false, false, TM>(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
         }
 #pragma unroll
-        for (int j = 0; j < LN_P; ++j) ln_count_chunk(in, lut, (uint32_t)(g * LN_P + j), buf[g & 1][j], cnt_a, cnt_t, c24);
+        for (int j = 0; j < LN_P; ++j)
+            ln_count_chunk(in, lut, (uint32_t)(g * LN_P + j), buf[g & 1][j], nrm, cnt_a, cnt_t, c24, capture, lane,
+                           nfl, fl_all, smp_all);
     }
 }
 
-/* Early exit of the lane path (round 5), for shallow blocks:
- * before any key is built, a count pass over a site's reads decides the sites
- * whose result needs no likelihood at all and writes their score; the others
- * are queued for ln_block.  Exact -- the reference's own outcome -- and never
- * taken when glf records are requested:
+#define SS_NEAR_K 3u                 /* non-reference contributing reads per sample the early exit evaluates */
+
+__device__ __forceinline__ uint32_t ln_ffbl(uint32_t x)
+{
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t ln_sel4(const uint32_t (&v)[4], uint32_t i)
+{
+    return i == 0u ? v[0] : i == 1u ? v[1] : i == 2u ? v[2] : v[3];
+}
+__device__ __forceinline__ float ln_sel4f(const float (&v)[4], uint32_t i)
+{
+    return i == 0u ? v[0] : i == 1u ? v[1] : i == 2u ? v[2] : v[3];
+}
+
+/* One sample of the early exit's near-reference test (see ln_classify):
+ * keys (descending after the sort) of its <= SS_NEAR_K non-reference
+ * contributing reads, 0 = none; c its contributing reads per group (the
+ * reference group's count included), c24 its contributing reads of
+ * minq >= 24.  True when sniper_glf2cns (sniper_maqcns.c:250-273) is proven to
+ * call the reference homozygote. */
+__device__ __forceinline__ bool ln_near_sample(uint32_t (&k)[SS_NEAR_K], const uint32_t (&c)[4], uint32_t c24,
+                                               uint32_t r, const ss_dev_model &m, const double *fk)
+{
+    static_assert(SS_NEAR_K == 3u, "the sort below is for three keys");
+    {   /* descending */
+        uint32_t a0 = max(k[0], k[1]), a1 = min(k[0], k[1]);
+        const uint32_t b1 = max(a1, k[2]), b2 = min(a1, k[2]);
+        k[0] = max(a0, b1);
+        k[1] = min(a0, b1);
+        k[2] = b2;
+    }
+    /* the non-reference groups' chains (sniper_maqcns.c:162-172): within a
+     * group the keys are walked in descending order, w counts per strand */
+    float es[4] = {0.0f, 0.0f, 0.0f, 0.0f}, fs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const char *fkb = reinterpret_cast<const char *>(fk);
+    uint32_t c24nr = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < SS_NEAR_K; ++i) {
+        const uint32_t key = k[i];
+        if (!__ballot(key != 0u)) break;
+        const uint32_t x = (key >> 13) & 3u;
+        const uint32_t minq = (key >> 5) & 0xffu;
+        const uint32_t q = max(minq, (key & 1u) << 2);        /* sniper_maqcns.c:165 */
+        uint32_t w = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < i; ++j) w += ((k[j] ^ key) & 0x6008u) == 0u ? 1u : 0u;   /* same group, strand */
+        const double fv = *reinterpret_cast<const double *>(fkb + 8u * (key ? w : (uint32_t)LN_FK_ZERO));
+        const float e0 = ln_sel4f(es, x), f0 = ln_sel4f(fs, x);
+        const float e1 = (float)((double)e0 + fv * (double)q);
+        const float f1 = (float)((double)f0 + fv);
+#pragma unroll
+        for (uint32_t b = 0; b < 4u; ++b) {
+            es[b] = b == x ? e1 : es[b];
+            fs[b] = b == x ? f1 : fs[b];
+        }
+        c24nr += key && minq >= 24u ? 1u : 0u;
+    }
+    const uint32_t tot = c[0] + c[1] + c[2] + c[3];          /* <= 128: no rescale (:178-182) */
+    /* the genotypes with the reference base, as geno_p (:184-214): t = 3 the
+     * homozygote, t < 3 the heterozygote with base x_t */
+    float pv[4];
+    uint32_t icv[4], ilv[4], c2v[4];
+    float ev[4];
+#pragma unroll
+    for (uint32_t t = 0; t < 4u; ++t) {
+        const uint32_t x = t < 3u ? t + (t >= r ? 1u : 0u) : r;
+        float e = 0.0f, f = 0.0f;
+        uint32_t c2 = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4u; ++i) {
+            const bool use = i != r && i != x;
+            e = use ? e + es[i] : e;
+            f = use ? f + fs[i] : f;
+            c2 += use ? c[i] : 0u;
+        }
+        const uint32_t be = (uint32_t)bar_e_fast(e, c2 ? f : 1.0f);
+        icv[t] = c2 ? (be << 16 | tot << 8 | c2) : 0u;
+        const uint32_t j0 = min(r, x), k0 = max(r, x);
+        ilv[t] = t < 3u ? (ln_sel4(c, j0) << 8 | ln_sel4(c, k0)) : 0u;
+        c2v[t] = c2;
+        ev[t] = e;
+    }
+    double cf[4], lv[4];
+#pragma unroll
+    for (uint32_t t = 0; t < 4u; ++t) {
+        cf[t] = ss_tab_coef(m)[icv[t]];
+        lv[t] = ss_tab_lhet(m)[ilv[t]];
+    }
+    const float esr = ss_tab_esr(m)[c24 - c24nr];
+    const float cmn = ss_tab_cmin(m)[tot];
+#pragma unroll
+    for (uint32_t t = 0; t < 4u; ++t) {
+        float v;
+        if (t == 3u) {
+            v = c2v[t] ? (float)((double)ev[t] + cf[t]) : 0.0f;
+        } else {
+            const double lh = -4.343 * lv[t];
+            v = c2v[t] ? (float)((lh + (double)ev[t]) + cf[t]) : (float)lh;
+        }
+        pv[t] = v < 0.0f ? 0.0f : v;
+    }
+    /* every genotype without the reference base has p >= esum[ref] + lh + coef
+     * >= lb (ss_capi.hip near_tables), and esum[ref] > every other esum, so
+     * the homozygote fix (:216-233) picks the reference homozygote's row and
+     * leaves it (its p is the smallest diagonal by more than 1); those
+     * genotypes then quantise above the reference homozygote */
+    const float lb = esr + cmn;
+    const float phr = pv[3];
+    const float min_p = min(min(phr, pv[0]), min(pv[1], pv[2]));
+    /* (bitwise: no short-circuit branches) */
+    bool ok = (esr > max(max(es[0], es[1]), max(es[2], es[3]))) & (lb - phr >= 3.0f) & (phr - min_p <= 250.0f);
+    const int lhr = (int)((double)(phr - min_p) + 0.5);
+#pragma unroll
+    for (uint32_t t = 0; t < 3u; ++t) {
+        const float d = pv[t] - min_p;
+        const int sc = ((double)d > 255.0 ? 255 : (int)((double)d + 0.5)) + m.q_r_int;
+        /* sniper_glf2cns takes the first minimum in genotype order: a
+         * heterozygote (x, r) with x < r comes before the homozygote */
+        ok = ok & (t < r ? sc > lhr : sc >= lhr);
+    }
+    return ok;
+}
+
+/* Early exit of the lane path (rounds 5-6), for blocks of
+ * shallow sites: before any key is built, a count pass over a site's reads
+ * decides the sites whose result needs no full likelihood computation and
+ * writes their score; the others are queued for ln_block.  Exact -- the
+ * reference's own outcome -- and never taken when glf records are requested:
  *   - ref char 'N' or an empty sample: -1 (somatic_sniper.c:127);
  *   - a reference code of 15 other than 'N' ('n', ...): 255, never an SNV
  *     candidate (:156);
- *   - reference A/C/G/T, every read of both samples on the reference base
- *     (bam_nt16_nt4_table semantics, sniper_maqcns.c:153-154: N/IUPAC reads
- *     count as A, '=' as the reference) and enough reads of minq >= 24: 255.
- *     Then in each sample the reference homozygote has p = 0 (tmp2 = 0,
- *     :196) and every other homozygote p = esum + coef[bar_e][n][n] with
- *     esum >= 24 * (fk[0] + .. + fk[c24 - 1]) (the walk visits the c24 reads
- *     of q >= 24 first, each with a weight fk[w] >= fk[k]); the host table
- *     SS_TAB_FAST holds, per read count n, the smallest c24 that makes that
- *     >= 1 for every bar_e and every n' <= n (ss_capi.hip fast_table), so
- *     those homozygotes quantise to lk >= 1, the heterozygotes score
- *     >= q_r >= 1 (SS_MF_FAST requires it), and sniper_glf2cns (:250-273)
- *     calls the reference homozygote in both samples: no candidate.
+ *   - reference A/C/G/T and at most SS_NEAR_K contributing reads per sample
+ *     off the reference base (round 6; round 5 took none): those reads are
+ *     loaded again (by the element bits of the count pass) and folded exactly,
+ *     which gives each sample's four genotypes with the reference base exactly
+ *     (their e sums skip the reference group, :188-208), and a lower bound for
+ *     the six without it (ss_capi.hip near_tables).  When the bounds put the
+ *     reference homozygote first in sniper_glf2cns in both samples, t1 == n1
+ *     and the site scores 255 (:156).
  * Returns true when it wrote the site's score. */
-__device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 *lut, uint32_t s, bool insite,
-                                            uint32_t end_t, uint32_t end_n)
+__device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 *lut, const double *fk, LaneLds &L,
+                                            uint32_t lane, uint32_t s, bool insite, uint32_t end_t, uint32_t end_n)
 {
     uint32_t ot = 0, ot1 = 0, on = 0, on1 = 0, refc = 'N';
     if (insite) {
@@ -1574,33 +1725,101 @@ __device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 
     const bool acgt = ref16 == 1u || ref16 == 2u || ref16 == 4u || ref16 == 8u;
     const bool cand = small && !done && acgt;
     if (__ballot(cand)) {
-        LaneIn in;
-        in.na = cand ? nt : 0u;
-        in.na4 = (in.na + 3u) & ~3u;
-        in.nb = cand ? nn : 0u;
-        in.nca = in.na4 >> 2;
-        asm("" : "+v"(in.nca));
-        in.nab = in.na4 + in.nb;
+        /* one count pass over both samples when every site fits the joint
+         * layout (the tumor's reads, padded to 4, then the normal's: <= 128
+         * elements, one 128-bit element set), else one pass per sample (as
+         * ln_block's separate mode) with a set each */
+        const uint32_t nt4 = (nt + 3u) & ~3u;
+        const bool joint = !__ballot(cand && nt4 + nn > LN_N);
         const uint32_t oa = cand ? ot : 0u, ob = cand ? on : 0u;
-        in.pa = a.reads_t + oa;
-        in.pb = a.reads_n + ob - in.na4;
-        in.la = ln_lut_row(1u + ref16);
-        in.lb = ln_lut_row(17u + ref16);
-        const uint32_t nch = wave_max((in.nab + 3u) >> 2);
-        /* as in ln_block: word loads when an x4 load could pass the end of the reads */
-        in.tail = ln_uniform(__ballot((uint64_t)oa + in.na4 > (uint64_t)end_t ||
-                                      (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4) ||
-                             end_t < 4u || end_n < 4u);
-        uint32_t cnt_a = 0, cnt_t = 0, c24 = 0;
-        if (in.tail) ln_count_pass<2>(in, lut, nch, cnt_a, cnt_t, c24);
-        else ln_count_pass<1>(in, lut, nch, cnt_a, cnt_t, c24);
-        const uint32_t sh = 8u * (uint32_t)__builtin_ctz(ref16 | 16u);   /* the reference base's count field */
-        const uint32_t cnt_b = cnt_t - cnt_a;
-        const uint32_t tot_a = (cnt_a & 0xffu) + (cnt_a >> 8 & 0xffu) + (cnt_a >> 16 & 0xffu) + (cnt_a >> 24);
-        const uint32_t tot_b = (cnt_b & 0xffu) + (cnt_b >> 8 & 0xffu) + (cnt_b >> 16 & 0xffu) + (cnt_b >> 24);
-        if (cand && tot_a == nt && tot_b == nn && ((cnt_a >> sh) & 0xffu) == nt && ((cnt_b >> sh) & 0xffu) == nn) {
-            const uint8_t *thr = ss_tab_fast(a.m);
-            if ((c24 & 0xffffu) >= thr[nt] && (c24 >> 16) >= thr[nn]) done = true;
+        uint32_t cnt_T = 0, cnt_N = 0, c24_T = 0, c24_N = 0;
+        /* chunks with an off-reference read, kept in the wave's record rows
+         * (free until ln_block): words in capture[slot][lane], element flags
+         * in fl_all (4 bits per slot), the sample in smp_all */
+        uint4 *capture = reinterpret_cast<uint4 *>(&L.rec[0][0]);
+        static_assert(sizeof(L.rec) >= SS_NEAR_SLOTS * 64 * sizeof(uint4), "capture slots fit the record rows");
+        uint32_t nfl = 0, fl_all = 0, smp_all = 0;
+        const uint32_t *p0a = a.reads_t + oa, *p0b = a.reads_n + ob - (cand ? nt4 : 0u), *p1 = a.reads_n + ob;
+        for (uint32_t pass = 0; pass < (joint ? 1u : 2u); ++pass) {
+            const bool nrm = pass == 1u;
+            LaneIn in;
+            in.na = cand ? (nrm ? nn : nt) : 0u;
+            in.na4 = (in.na + 3u) & ~3u;
+            in.nb = joint && cand ? nn : 0u;
+            in.nca = in.na4 >> 2;
+            asm("" : "+v"(in.nca));
+            in.nab = in.na4 + in.nb;
+            in.pa = nrm ? p1 : p0a;
+            in.pb = joint ? p0b : in.pa;               /* a pass of one sample: chunks past its reads load the next sites' */
+            in.la = ln_lut_row(1u + (nrm ? 16u : 0u) + ref16);
+            in.lb = ln_lut_row(17u + ref16);
+            const uint32_t nch = wave_max((in.nab + 3u) >> 2);
+            /* as in ln_block: word loads when an x4 load could pass the end of the reads */
+            const uint32_t oo = nrm ? ob : oa, eo = nrm ? end_n : end_t;
+            in.tail = ln_uniform(__ballot(joint ? ((uint64_t)oa + in.na4 > (uint64_t)end_t ||
+                                                   (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4)
+                                                : (uint64_t)oo + 4u * nch > (uint64_t)eo) ||
+                                 end_t < 4u || end_n < 4u);
+            uint32_t cnt_a = 0, cnt_t = 0, c24 = 0;
+            if (in.tail) ln_count_pass<2>(in, lut, nch, nrm ? 1u : 0u, cnt_a, cnt_t, c24, capture, lane, nfl, fl_all, smp_all);
+            else ln_count_pass<1>(in, lut, nch, nrm ? 1u : 0u, cnt_a, cnt_t, c24, capture, lane, nfl, fl_all, smp_all);
+            if (!nrm) {
+                cnt_T = cnt_a;
+                cnt_N = cnt_t - cnt_a;                 /* joint: the rest */
+                c24_T = c24 & 0xffffu;
+                c24_N = c24 >> 16;
+            } else {
+                cnt_N = cnt_a;
+                c24_N = c24 & 0xffffu;
+            }
+        }
+        const uint32_t r = (uint32_t)__builtin_ctz(ref16 | 16u);     /* the reference base (0..3 for cand) */
+        uint32_t ca[4], cb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ca[i] = (cnt_T >> (8 * i)) & 0xffu;
+            cb[i] = (cnt_N >> (8 * i)) & 0xffu;
+        }
+        const uint32_t ma = ca[0] + ca[1] + ca[2] + ca[3] - ln_sel4(ca, r);
+        const uint32_t mb = cb[0] + cb[1] + cb[2] + cb[3] - ln_sel4(cb, r);
+        const bool ok = cand && ma <= SS_NEAR_K && mb <= SS_NEAR_K;
+        if (__ballot(ok)) {
+            /* the off-reference reads from the captured chunks, in element
+             * order (the tumor's first); at most 2 SS_NEAR_K of them matter */
+            if (!ok) fl_all = 0u;
+            uint32_t key[2 * SS_NEAR_K];
+            const uint32_t *cw = reinterpret_cast<const uint32_t *>(capture);
+#pragma unroll
+            for (uint32_t i = 0; i < 2u * SS_NEAR_K; ++i) {
+                const bool has = fl_all != 0u;
+                const uint32_t bpos = ln_ffbl(fl_all) & 31u;
+                fl_all &= fl_all - 1u;
+                const uint32_t slot = bpos >> 2;
+                const uint32_t rd = has ? cw[(slot * 64u + lane) * 4u + (bpos & 3u)] : 0u;
+                const uint32_t row = ln_lut_row(((smp_all >> slot) & 1u ? 17u : 1u) + ref16);
+                uint32_t minq;
+                asm("v_min_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_1"
+                    : "=v"(minq) : "v"(rd));
+                const uint32_t ex = reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(lut) +
+                                                                   (((rd >> 13) & 0xf8u) ^ row))->x;
+                /* the key build's 16-bit key (ln_chunk), minq in 8 bits (5..12) */
+                const uint32_t kk = (ex & 0xffffu) | minq << 5 | ((rd >> 13) & 6u) | ln_nz(rd & 0x3f00u);
+                key[i] = has ? kk : 0u;
+            }
+            uint32_t kt[SS_NEAR_K], kn[SS_NEAR_K];
+#pragma unroll
+            for (uint32_t i = 0; i < SS_NEAR_K; ++i) {
+                kt[i] = i < ma ? key[i] : 0u;
+                const uint32_t j = ma + i;                   /* <= 2K - 1 */
+                const uint32_t kj = j == 0u ? key[0] : j == 1u ? key[1] : j == 2u ? key[2] : j == 3u ? key[3]
+                                  : j == 4u ? key[4] : key[5];
+                kn[i] = i < mb ? kj : 0u;
+            }
+            /* both samples on every lane (no divergent region; a lane that
+             * is not ok has no keys and its answer is dropped) */
+            const bool okt = ln_near_sample(kt, ca, c24_T, r, a.m, fk);
+            const bool okn = ln_near_sample(kn, cb, c24_N, r, a.m, fk);
+            done = done || (ok & okt & okn);
         }
     }
     if (done) kernarg_args().score[s] = sc;
@@ -1666,7 +1885,7 @@ void ss_score_main(ss_score_args a)
                 shallow = breads <= SS_EARLY_MAX_READS * (s1 - s0);
             }
             if (shallow) {
-                const bool need = insite && !ln_classify(kernarg_args(), lut, s, insite, end_t, end_n);
+                const bool need = insite && !ln_classify(kernarg_args(), lut, fk, L, lane, s, insite, end_t, end_n);
                 const uint64_t m = __ballot(need);
                 if (need)
                     queue[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -2827,9 +3046,12 @@ __global__ __launch_bounds__(SS_DEEP_BLOCK) void ss_score_deep(ss_score_args a)
 /* --------------------------------------------------------------------------
  * Synthetic generator (device twin of ss_synth.c; same ss_synth_core.h code).
  * ------------------------------------------------------------------------ */
+/* depths per site, and their 64-bit totals into sums[0..1] (the host checks
+ * that the 32-bit read offsets cannot wrap) */
 __global__ void ss_synth_depth_kernel(ss_synth_k_t k, uint64_t first, uint64_t n, uint8_t *ref,
-                                      uint32_t *dt, uint32_t *dn)
+                                      uint32_t *dt, uint32_t *dn, unsigned long long *sums)
 {
+    unsigned long long st = 0, sn = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         ss_site_draw_t d;
@@ -2838,8 +3060,18 @@ __global__ void ss_synth_depth_kernel(ss_synth_k_t k, uint64_t first, uint64_t n
         ref[i] = d.ref_char;
         for (j = c = 0; j < d.raw_tumor; ++j) c += (uint32_t)ss_synth_read(&k, first + i, &d, 0, j, &r);
         dt[i] = c;
+        st += c;
         for (j = c = 0; j < d.raw_normal; ++j) c += (uint32_t)ss_synth_read(&k, first + i, &d, 1, j, &r);
         dn[i] = c;
+        sn += c;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        st += __shfl_xor(st, o);
+        sn += __shfl_xor(sn, o);
+    }
+    if (__lane_id() == 0) {
+        atomicAdd(&sums[0], st);
+        atomicAdd(&sums[1], sn);
     }
 }
 
@@ -2928,13 +3160,13 @@ int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int de
 }
 
 int ss_launch_synth_depth(const ss_synth_k_t &k, uint64_t first, uint64_t n, uint8_t *ref,
-                          uint32_t *dt, uint32_t *dn, hipStream_t s)
+                          uint32_t *dt, uint32_t *dn, unsigned long long *sums, hipStream_t s)
 {
     uint64_t blocks = (n + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(ss_synth_depth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, k, first, n,
-                       ref, dt, dn);
+                       ref, dt, dn, sums);
     return (int)hipGetLastError();
 }
 

@@ -1,75 +1,109 @@
-"""The main kernel's early exit (ss_kernels.hip ln_classify)
-scores an all-reference site 255 without computing likelihoods when each
-sample has at least thr[n] reads of minq >= 24, thr from the host table
-(ss_capi.hip fast_table: the smallest c24 with
-24 * (m[0] + .. + m[c24 - 1]) * (1 - 1e-4) + min coef[q][n'][n'] >= 1 over
-q in [4, 63], n' <= n, m[k] = min(fk[0 .. k]), enabled only with q_r >= 1).
-The running minimum keeps the bound sound when fk increases (theta > 1, which
-the reference's -T accepts: main.c:83 has no range check).
+"""The main kernel's early exit (ss_kernels.hip ln_classify /
+ln_near_sample) scores a site 255 without its full likelihoods when, in both
+samples, at most three contributing reads lie off the reference base and the
+bounds of ss_capi.hip near_tables prove that sniper_glf2cns calls the
+reference homozygote (tests/near_exit_model.py restates both).
 
-This CPU test restates that table from the oracle's own model tables and
-checks the rule's soundness against the oracle (pinned to the compiled
-reference by test_oracle_golden.py) on the sites that press it hardest, at
-every depth 1 .. 128: exactly thr[n] reads of q 24 (the smallest weight the
-bound assumes), every other read at the lowest contributing quality (q 4) or
-not contributing at all, one strand or alternating strands, every reference
-base, under option sets that change the model tables.  No GPU."""
+These CPU tests check that rule's soundness against the oracle (pinned to the
+compiled reference by test_oracle_golden.py): every site the model exits must
+score 255 in the oracle.  The sites press the bound hardest -- few reads of
+q >= 24 on the reference (exactly the smallest weight the bound assumes), the
+rest at q 4 or not contributing, one strand or alternating strands, and up to
+three off-reference reads of every quality, base, strand and baseQ tie-break
+class -- under option sets that change the model tables, including theta > 1
+(fk increasing; the reference's -T has no range check, main.c:83).  No GPU."""
 import numpy as np
 import pytest
 
+from near_exit_model import NEAR_K, near_exit, near_tables
 
-def fast_thresholds(fk, coef, q_r):
-    """ss_capi.hip fast_table, restated: 255 = the exit never applies."""
-    thr = np.full(256, 255, np.int64)
-    if q_r < 1:
-        return thr
-    F = np.zeros(130)
-    run_min = fk[0]
-    for k in range(129):
-        run_min = min(run_min, fk[min(k, 255)])
-        F[k + 1] = F[k] + run_min
-    cm = 1e300
-    for n in range(1, 129):
-        cm = min(cm, min(coef[q << 16 | n << 8 | n] for q in range(4, 64)))
-        for c in range(1, n + 1):
-            if 24.0 * F[c] * (1.0 - 1e-4) + cm >= 1.0:
-                thr[n] = c
-                break
-    return thr
+OPTS = [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"], ["-T", "1.2"]]
+REF16 = {"A": 1, "C": 2, "G": 4, "T": 8}
 
 
-def _sample(pkg, base, n, c24, rest_bq, alternate):
-    # alternating strands give the q-24 reads the weights fk[0], fk[0], fk[1],
-    # fk[1], ...: the smallest ones when fk increases (theta > 1)
-    reads = [pkg.pack_read(60, 24, base, (i & 1) if alternate else 0) for i in range(c24)]
-    reads += [pkg.pack_read(60, rest_bq, base, (i & 1) if alternate else 0) for i in range(n - c24)]
-    return reads
-
-
-@pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"],
-                                  ["-T", "1.2"]])
-def test_early_exit_thresholds_sound(pkg, oracle, opts):
-    o = oracle.Oracle(oracle.opts_to_params(list(opts)))
-    t = o.tables()
-    thr = fast_thresholds(t["fk"], t["coef"], t["q_r"])
-    if t["q_r"] < 1:
-        pytest.skip("q_r < 1: the exit is disabled")
-    assert (thr[1:129] < 255).any(), "the exit would never apply"
+def _pressing_sites(pkg, rng, n_sites):
     sites = []
-    for n in range(1, 129):
-        if thr[n] == 255:
-            continue
-        for base, refc in ((1, "A"), (2, "C"), (4, "G"), (8, "T")):
-            for rest_bq, alternate in ((4, False), (4, True), (0, True)):
-                t_reads = _sample(pkg, base, n, int(thr[n]), rest_bq, alternate)
-                m = max(1, n // 2)          # the normal at another depth, at its own threshold
-                if thr[m] == 255:
-                    continue
-                n_reads = _sample(pkg, base, m, int(thr[m]), rest_bq, not alternate)
-                sites.append((refc, t_reads, n_reads))
-    assert len(sites) > 1000
+    for _ in range(n_sites):
+        refc = "ACGT"[rng.integers(4)]
+        r = "ACGT".index(refc)
+        smp = []
+        for _s in range(2):
+            n = int(rng.integers(1, 129))
+            c24 = int(min(n, rng.integers(0, 14)))
+            alt = bool(rng.integers(2))
+            rest_bq = int(rng.choice([4, 4, 0, 7, 23, 130]))
+            reads = [pkg.pack_read(60, 24, 1 << r, (i & 1) if alt else 0) for i in range(c24)]
+            reads += [pkg.pack_read(60 if rest_bq else int(rng.integers(0, 60)), rest_bq, 1 << r,
+                                    (i & 1) if alt else int(rng.integers(2))) for i in range(n - c24)]
+            m = int(rng.integers(0, NEAR_K + 2))          # sometimes one more than the exit takes
+            for _j in range(m):
+                b = int(rng.integers(4))
+                nt16 = int(rng.choice([1 << b, 15, 5, 0])) if b != r else 15
+                bq = int(rng.choice([int(rng.integers(1, 64)), int(rng.integers(64, 256)), 2, 3, 64, 128]))
+                mq = int(rng.choice([60, int(rng.integers(0, 256)), 2]))
+                reads.insert(int(rng.integers(len(reads) + 1)),
+                             pkg.pack_read(mq, bq, nt16, int(rng.integers(2))))
+            smp.append(reads[:128])
+        sites.append((refc, smp[0], smp[1]))
+    return sites
+
+
+def _ref16(rc):
+    return REF16.get((rc if isinstance(rc, str) else chr(rc)).upper(), 15)
+
+
+def _check(pkg, oracle, o, sites, t, tabs, min_exits):
+    exits = np.array([near_exit(_ref16(rc), rt, rn, tabs, t) for rc, rt, rn in sites])
     batch = pkg.Batch.from_sites(sites)
     score, _, _ = o.score_batch(batch.ref, batch.off_tumor, batch.off_normal, batch.reads_tumor,
                                 batch.reads_normal, want_glf=False)
-    bad = np.nonzero(score != 255)[0]
-    assert bad.size == 0, f"{bad.size} all-reference sites at the threshold not scored 255, first {bad[:5]}"
+    bad = np.nonzero(exits & (score != 255))[0]
+    assert bad.size == 0, f"{bad.size} sites the exit scores 255 score otherwise, first {bad[:5]} {score[bad[:5]]}"
+    assert exits.sum() >= min_exits, f"the exit took only {exits.sum()} of {len(sites)} sites"
+    assert (~exits).sum() > 0
+    return exits
+
+
+@pytest.mark.parametrize("opts", OPTS)
+def test_near_exit_sound_pressing(pkg, oracle, opts):
+    o = oracle.Oracle(oracle.opts_to_params(list(opts)))
+    t = o.tables()
+    tabs = near_tables(t["fk"], t["coef"], t["lhet"], t["q_r"])
+    if tabs is None:
+        pytest.skip("q_r < 1: the exit is disabled")
+    rng = np.random.default_rng(20260 + len(opts))
+    sites = _pressing_sites(pkg, rng, 2500)
+    _check(pkg, oracle, o, sites, t, tabs, min_exits=150)
+
+
+@pytest.mark.parametrize("opts", [[], ["-T", "1.2"]])
+def test_near_exit_sound_noisy_synth(pkg, oracle, opts):
+    """synthetic pileups at 10x the default error rate, with germline and
+    somatic sites, at 30x/20x: most sites carry off-reference reads"""
+    o = oracle.Oracle(oracle.opts_to_params(list(opts)))
+    t = o.tables()
+    tabs = near_tables(t["fk"], t["coef"], t["lhet"], t["q_r"])
+    b = pkg.synth_batch_host(pkg.Synth.default(30, 20, p_error=0.1, p_somatic=0.02, p_germline=0.02), 0, 2500)
+    sites = [b.site(i) for i in range(b.n_sites)]
+    _check(pkg, oracle, o, sites, t, tabs, min_exits=200)
+
+
+def test_near_tables_bound_esum(oracle):
+    """esr[c] never exceeds the smallest esum of c q-24 reads: the reads
+    alternate strands (weights fk[0], fk[0], fk[1], ..) or keep one (fk[0],
+    fk[1], ..), whichever is smaller, with the float accumulation of the fold"""
+    for opts in OPTS:
+        o = oracle.Oracle(oracle.opts_to_params(list(opts)))
+        t = o.tables()
+        tabs = near_tables(t["fk"], t["coef"], t["lhet"], t["q_r"])
+        if tabs is None:
+            continue
+        fk = t["fk"]
+        for c in range(1, 129):
+            lo = None
+            for alt in (False, True):
+                e = np.float32(0)
+                for i in range(c):
+                    e = np.float32(float(e) + float(fk[i // 2 if alt else i]) * 24.0)
+                lo = e if lo is None else min(lo, e)
+            assert tabs[0][c] <= lo, (opts, c, tabs[0][c], lo)

@@ -470,18 +470,39 @@ def test_all_reference_sites_parity(pkg, oracle, opts):
 @pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"]])
 def test_early_exit_mixed_blocks(pkg, oracle, opts):
     """The main kernel's early exit is decided per 64-site block (mean depth
-    <= 72 reads per site, in a batch of mean <= 80): shallow blocks (25x/20x)
-    and deep ones (60x/45x) alternate, so the undecided sites of shallow
+    <= 256 reads per site, in a batch of mean <= 264): shallow blocks
+    (25x/20x) and deep ones (150x/120x, many of their sites past the lane
+    path's 128 reads per sample) alternate, so the undecided sites of shallow
     blocks wait in the wave's queue while deep blocks are scored directly,
     and the queue's last, partial batch is scored at the end."""
     sh = pkg.synth_batch_host(pkg.Synth.default(25, 20, seed=91, **EXOTIC), 0, 64 * 40)
-    dp = pkg.synth_batch_host(pkg.Synth.default(60, 45, seed=92, **EXOTIC), 0, 64 * 40 + 17)
+    dp = pkg.synth_batch_host(pkg.Synth.default(150, 120, seed=92, **EXOTIC), 0, 64 * 40 + 17)
     sites = []
     for b in range(40):
         sites += [sh.site(64 * b + i) for i in range(64)]
         sites += [dp.site(64 * b + i) for i in range(64)]
     sites += [dp.site(64 * 40 + i) for i in range(17)]
     assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), opts)
+
+
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"],
+                                  ["-T", "1.2"]])
+def test_near_exit_parity(pkg, oracle, opts):
+    """The early exit's near-reference test (round 6: up to three
+    off-reference reads per sample) on the sites that press its
+    bounds hardest (tests/test_early_exit_bound.py: few q-24 reference reads,
+    off-reference reads of every quality, base, strand and baseQ class, some
+    samples with one read more than the exit takes) and on synthetic pileups
+    at 10x the default error rate with germline and somatic sites, at depths
+    on both sides of the lane path's limits: every score, call and glf record
+    against the oracle, with glf records (no exit) and without (exit)."""
+    from test_early_exit_bound import _pressing_sites
+    rng = np.random.default_rng(4242 + len(opts))
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(_pressing_sites(pkg, rng, 6000)), opts)
+    for lt, ln in ((30, 20), (60, 30), (100, 60), (120, 110)):
+        b = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=55 + lt, p_error=0.1, p_somatic=0.02,
+                                                   p_germline=0.02), 0, 6000)
+        assert_parity(pkg, oracle, b, opts)
 
 
 @pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"], ["-T", "1.2"]])
