@@ -263,15 +263,37 @@ def pmc_child(args):
     ctx.close()
 
 
+def _launch_groups(rows, names):
+    """rocprofv3 records of the kernels `names` (a launch's dispatches of its
+    kernel class in launch order, the last name closing a launch: the triage
+    kernel, then the main kernel) grouped per launch, in dispatch order:
+    [(dispatch ids, records)]"""
+    by_id = {}
+    for name, did, rec in rows:
+        by_id.setdefault(did, (name, []))[1].append(rec)
+    groups, cur_ids, cur = [], [], []
+    for did in sorted(by_id):
+        name, recs = by_id[did]
+        cur_ids.append(did)
+        cur.extend(recs)
+        if name == names[-1]:
+            groups.append((cur_ids, cur))
+            cur_ids, cur = [], []
+    return groups
+
+
 def live_counters(args, kernel="ss_score_main"):
     """rocprofv3 --pmc passes over a child that scores the bench's own batch
-    (same sites, depths, seed): per-launch means of `kernel`'s counters, the
-    first launch dropped (cold tables).  None when rocprofv3 is missing or a
-    pass fails -- the timed result never depends on it."""
+    (same sites, depths, seed): per-launch means of `kernel`'s counters ('a+b':
+    a kernel class of several kernels, summed per launch), the first launch
+    dropped (cold tables).  None when rocprofv3 is missing or a pass fails --
+    the timed result never depends on it."""
     import csv
     import re
     import shutil
     import tempfile
+    names = kernel.split("+")
+    kpat = re.compile("(" + "|".join(re.escape(k) for k in names) + r")[<(]")
     exe = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
     if exe is None:
         return None
@@ -311,13 +333,14 @@ def live_counters(args, kernel="ss_score_main"):
                 if want in fs:
                     path = os.path.join(dp, want)
             if counters is None and r.returncode == 0 and path is not None:
-                durs = []
+                rows = []
                 with open(path) as f:
                     for row in csv.DictReader(f):
-                        if re.search(re.escape(kernel) + r"[<(]", row["Kernel_Name"]):
-                            durs.append((int(row["Dispatch_Id"]),
+                        mk = kpat.search(row["Kernel_Name"])
+                        if mk:
+                            rows.append((mk.group(1), int(row["Dispatch_Id"]),
                                          float(row["End_Timestamp"]) - float(row["Start_Timestamp"])))
-                durs = [d for _, d in sorted(durs)]
+                durs = [sum(g) for _, g in _launch_groups(rows, names)]
                 n_pass = len(durs) // max(1, args.pmc_launches)
                 warm = durs[n_pass:] or durs
                 vals["_kt"] = {"all_dispatches_ms": round(float(np.mean(durs)) / 1e6, 4) if durs else None,
@@ -330,14 +353,22 @@ def live_counters(args, kernel="ss_score_main"):
             if r.returncode != 0 or path is None:
                 print(f"bench: PMC pass {counters} failed (rc {r.returncode}): {r.stderr[-500:]}", file=sys.stderr)
                 return None
-            per = {}
+            rows = []
             with open(path) as f:
                 for row in csv.DictReader(f):
-                    if re.search(re.escape(kernel) + r"[<(]", row["Kernel_Name"]):
-                        d = per.setdefault(int(row["Dispatch_Id"]), {})
-                        d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
-                        # the dispatch's duration in this same profiled pass (ns)
-                        d["_dur_ns"] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+                    mk = kpat.search(row["Kernel_Name"])
+                    if mk:
+                        rows.append((mk.group(1), int(row["Dispatch_Id"]),
+                                     (row["Counter_Name"], float(row["Counter_Value"]),
+                                      float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))))
+            dispatch_ns = {did: dns for _, did, (_, _, dns) in rows}
+            per = {}
+            for gi, (ids, recs) in enumerate(_launch_groups(rows, names)):
+                d = per.setdefault(gi, {})
+                for cn, cv, _ in recs:
+                    d[cn] = d.get(cn, 0.0) + cv
+                # the launch's duration in this same profiled pass (ns): its dispatches' durations summed
+                d["_dur_ns"] = float(sum(dispatch_ns[i] for i in ids))
             # one pass = one launch per batch; the first pass (cold tables) is dropped
             n_pass = len(per) // max(1, args.pmc_launches)
             ds = sorted(per)[n_pass:] or sorted(per)
@@ -796,7 +827,10 @@ def main():
         "ranks": ranks,
         "roofline": {
             "bound": "hbm",
-            "kernel": {"main": "ss_score_main", "wide": "ss_score_group", "deep": "ss_score_deep"}[dom],
+            # the main class: the triage kernel (run when no glf records are
+            # requested) and the main kernel, summed per launch
+            "kernel": {"main": "ss_score_triage+ss_score_main", "wide": "ss_score_group",
+                       "deep": "ss_score_deep"}[dom],
             "achieved": round(achieved, 2) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -53,6 +53,7 @@ struct ss_ctx {
     uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6..7] listed
                                  entries | segments << 32, [8] the group kernel's chunk counter,
                                  [9] the deep kernel's chunk counter, [10] deep3 count,
+                                 [11] the triage list's count,
                                  [12..15] the device generator's read totals (2 x u64),
                                  [16..21] the table fingerprint (3 x u64) */
     uint32_t *d_deep_list;
@@ -510,9 +511,9 @@ extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double
     return SS_OK;
 }
 
-/* the deep list buffer holds three lists of deep_cap entries: the main
- * kernel's per-wave segments (deep), the group kernel's overflow (deep2) and
- * the deep kernel's (deep3).
+/* the deep list buffer holds four lists of deep_cap entries: the main
+ * kernel's per-wave segments (deep), the group kernel's overflow (deep2), the
+ * deep kernel's (deep3) and the triage kernel's undecided sites (tri).
  * Grown for a batch larger than any before (by at least half, so a run of
  * growing batches allocates O(log) times); the old list may still be read by
  * the context's previous launch, so it is retired, not reused, until
@@ -526,7 +527,7 @@ static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
     if (cap < n_sites) return SS_E_INVAL;
     dev_release(c, *(void **)&c->d_deep_list, false);
     c->deep_cap = 0;
-    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 3 * cap * sizeof(uint32_t), s)) return rc;
+    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 4 * cap * sizeof(uint32_t), s)) return rc;
     c->deep_cap = (uint32_t)cap;
     return SS_OK;
 }
@@ -584,8 +585,9 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     const int wide_grid = (int)std::min<uint64_t>((uint64_t)c->n_cu, wg_need);
     if ((rc = ensure_grp_cap(c, (uint32_t)wide_grid, s))) return rc;
     /* counters: deep2, listed segments and entries, the group and deep
-     * kernels' next chunks, deep3 (err is sticky until ss_ctx_check) */
-    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 6 * sizeof(uint32_t), s));
+     * kernels' next chunks, deep3, the triage list (err is sticky until
+     * ss_ctx_check) */
+    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 7 * sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
     memset(&a, 0, sizeof(a));
@@ -615,6 +617,11 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.deep_acc = reinterpret_cast<unsigned long long *>(c->d_counters + 6);   /* 8-byte aligned */
     a.wide_next = c->d_counters + 8;
     a.grp_rec = c->d_grp_rec;
+    /* the triage kernel's early exit writes no glf records and needs the
+     * host's bound tables (near_tables) */
+    const bool triage = o->glf == nullptr && c->fast_ok;
+    a.tri_list = triage ? c->d_deep_list + 3 * (size_t)c->deep_cap : nullptr;
+    a.tri_count = c->d_counters + 11;
     a.err = c->d_counters + 2;
     a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;
@@ -638,7 +645,11 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
         evs = c->ev->data() + SS_EV_PER_LAUNCH * c->n_logged;
         ++c->n_logged;
     }
-    int e = ss_launch_score(a, (int)blocks, wide_grid, deep_grid, wild_grid, s, evs);
+    /* triage: 8 waves per workgroup, grid-strided over the 64-site blocks */
+    const uint64_t tri_wpb = SS_TRIAGE_BLOCK / 64;
+    const int triage_grid = (int)std::min<uint64_t>((site_blocks + tri_wpb - 1) / tri_wpb,
+                                                    (uint64_t)c->n_cu * SS_TRIAGE_GRID_PER_CU);
+    int e = ss_launch_score(a, triage_grid, (int)blocks, wide_grid, deep_grid, wild_grid, s, evs);
     if (e != 0) return SS_E_HIP;
     HIPCHK(hipEventRecord(c->done, s));
     c->launched = 1;

@@ -1480,25 +1480,35 @@ __device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, boo
     wave_sync();
 }
 
-/* the early exit's count pass over chunk c (ln_classify): per sample the
- * contributing reads' group counts (8-bit fields, as the key build's) and its
- * contributing reads of minq >= 24.  A chunk with a contributing read whose
- * group is not the reference base's (the lookup table's bit 31) is kept for
- * the near-reference test: its four words go to the lane's LDS slot nfl
- * (capture[nfl][lane], at most SS_NEAR_SLOTS), their flags to bits 4 nfl of
- * fl_all and its sample (sb) to bit nfl of smp_all. */
-#define SS_NEAR_SLOTS 6u
-__device__ __forceinline__ void ln_count_chunk(const LaneIn &in, const uint2 *lut, uint32_t c, const uint32_t (&x)[4],
-                                               uint32_t nrm, uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24,
-                                               uint4 *capture, uint32_t lane, uint32_t &nfl, uint32_t &fl_all,
-                                               uint32_t &smp_all)
+/* The early exit's count pass (the triage kernel, round 6) reads a site's
+ * reads with TG lanes: the site's joint element list -- the tumor's reads,
+ * padded to 4, then the normal's -- in 4-read chunks, lane j of the site's
+ * group taking chunks j, j + TG, ..., so one load instruction reads TG x 16
+ * contiguous bytes of each of 64 / TG sites.  (Lane per site, every load
+ * instruction touched 64 lines: the texture address and data units were busy
+ * 83% / 94% of the kernel's cycles at C4) */
+#define TG 8u                        /* lanes per site in the count pass */
+#define SS_NEAR_SLOTS 4u             /* captured chunks per site: more means more than four off-reference reads */
+
+/* per wave: a round's per-site totals and the sites' captured chunks */
+struct TriLds {
+    uint4    cap[64][SS_NEAR_SLOTS];         /* chunks with an off-reference read, element order */
+    uint32_t capf[64];                       /* per slot (byte): its element flags | 16 for the normal's */
+    uint32_t cnt_t[64], cnt_n[64];           /* contributing reads per group (8-bit fields) */
+    uint32_t c24[64];                        /* contributing reads of minq >= 24: tumor | normal << 16 */
+    uint32_t nfl[64];                        /* chunks captured (past SS_NEAR_SLOTS: some lost) */
+};
+
+/* one chunk of the count pass: per sample the contributing reads' group
+ * counts and its reads of minq >= 24 (lim: elements of the chunk that are
+ * reads); returns the element flags of the contributing reads whose group is
+ * not the reference base's (the lookup table's bit 31) */
+__device__ __forceinline__ uint32_t tri_chunk(const uint2 *lut, const uint32_t (&x)[4], int lim, uint32_t row, bool fa,
+                                              uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24)
 {
-    const bool fa = c < in.nca;
-    const int lim = (int)(fa ? in.na : in.nab) - (int)(4u * c);
     uint32_t valid, vl;
     asm("v_med3_i32 %0, %1, 0, 4" : "=v"(vl) : "v"(lim));
     asm("v_bfm_b32 %0, %1, 0" : "=v"(valid) : "v"(vl));
-    const uint32_t row = fa ? in.la : in.lb;
     uint32_t minq[4];
     uint2 ent[4];
 #pragma unroll
@@ -1522,38 +1532,17 @@ __device__ __forceinline__ void ln_count_chunk(const LaneIn &in, const uint2 *lu
     cnt_t += cc;
     cnt_a += fa ? cc : 0u;
     c24 += fa ? q : q << 16;
-    if (fl != 0u && nfl < SS_NEAR_SLOTS) {
-        capture[nfl * 64u + lane] = make_uint4(x[0], x[1], x[2], x[3]);
-        fl_all |= fl << (4u * nfl);
-        smp_all |= (nrm | (fa ? 0u : 1u)) << nfl;
-        ++nfl;
-    }
+    return fl;
 }
 
-/* the count pass over a block's chunks: groups of LN_P chunk loads in flight,
- * as in ln_keys, the tail mode fixed per instantiation (TM, ln_load) */
-template <int TM>
-__device__ __forceinline__ void ln_count_pass(const LaneIn &in, const uint2 *lut, uint32_t nch, uint32_t nrm,
-                                              uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24, uint4 *capture,
-                                              uint32_t lane, uint32_t &nfl, uint32_t &fl_all, uint32_t &smp_all)
+/* sum over the TG = 8 lanes of a site's group (DPP: quad_perm xor 1, xor 2,
+ * then row_half_mirror, which pairs lane i with 7 - i of the other quad) */
+__device__ __forceinline__ uint32_t tri_gsum(uint32_t v)
 {
-    uint32_t buf[2][LN_P][4];
-    if (nch > 0u) {
-#pragma unroll
-        for (int j = 0; j < LN_P; ++j) ln_load<false, false, TM>(in, (uint32_t)j, buf[0][j]);
-    }
-#pragma unroll
-    for (int g = 0; g < LN_C / LN_P; ++g) {
-        if ((uint32_t)(g * LN_P) >= nch) break;
-        if (g + 1 < LN_C / LN_P && (uint32_t)((g + 1) * LN_P) < nch) {
-#pragma unroll
-            for (int j = 0; j < LN_P; ++j) ln_load<false, false, TM>(in, (uint32_t)((g + 1) * LN_P + j), buf[(g + 1) & 1][j]);
-        }
-#pragma unroll
-        for (int j = 0; j < LN_P; ++j)
-            ln_count_chunk(in, lut, (uint32_t)(g * LN_P + j), buf[g & 1][j], nrm, cnt_a, cnt_t, c24, capture, lane,
-                           nfl, fl_all, smp_all);
-    }
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);    /* quad_perm [1,0,3,2] */
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);    /* quad_perm [2,3,0,1] */
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);   /* row_half_mirror */
+    return v;
 }
 
 #define SS_NEAR_K 3u                 /* non-reference contributing reads per sample the early exit evaluates */
@@ -1574,7 +1563,7 @@ __device__ __forceinline__ float ln_sel4f(const float (&v)[4], uint32_t i)
     return i == 0u ? v[0] : i == 1u ? v[1] : i == 2u ? v[2] : v[3];
 }
 
-/* One sample of the early exit's near-reference test (see ln_classify):
+/* One sample of the early exit's near-reference test (see tri_block):
  * keys (descending after the sort) of its <= SS_NEAR_K non-reference
  * contributing reads, 0 = none; c its contributing reads per group (the
  * reference group's count included), c24 its contributing reads of
@@ -1683,25 +1672,26 @@ __device__ __forceinline__ bool ln_near_sample(uint32_t (&k)[SS_NEAR_K], const u
     return ok;
 }
 
-/* Early exit of the lane path (rounds 5-6), for blocks of
- * shallow sites: before any key is built, a count pass over a site's reads
- * decides the sites whose result needs no full likelihood computation and
- * writes their score; the others are queued for ln_block.  Exact -- the
- * reference's own outcome -- and never taken when glf records are requested:
+/* Early exit of the lane path (rounds 5-6), the triage
+ * kernel's work for one block of 64 sites (lane = site): a count pass over
+ * the sites' reads decides the sites whose result needs no full likelihood
+ * computation and writes their score; the others are returned (false) and
+ * listed for the main kernel.  Exact -- the reference's own outcome -- and
+ * never taken when glf records are requested:
  *   - ref char 'N' or an empty sample: -1 (somatic_sniper.c:127);
  *   - a reference code of 15 other than 'N' ('n', ...): 255, never an SNV
  *     candidate (:156);
- *   - reference A/C/G/T and at most SS_NEAR_K contributing reads per sample
- *     off the reference base (round 6; round 5 took none): those reads are
- *     loaded again (by the element bits of the count pass) and folded exactly,
+ *   - reference A/C/G/T, at most 128 reads per sample and at most SS_NEAR_K
+ *     contributing reads per sample off the reference base (round 6; round 5
+ *     took none): those reads are kept from the count pass and folded exactly,
  *     which gives each sample's four genotypes with the reference base exactly
  *     (their e sums skip the reference group, :188-208), and a lower bound for
  *     the six without it (ss_capi.hip near_tables).  When the bounds put the
  *     reference homozygote first in sniper_glf2cns in both samples, t1 == n1
  *     and the site scores 255 (:156).
  * Returns true when it wrote the site's score. */
-__device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 *lut, const double *fk, LaneLds &L,
-                                            uint32_t lane, uint32_t s, bool insite, uint32_t end_t, uint32_t end_n)
+__device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *lut, const double *fk, TriLds &T,
+                                          uint32_t lane, uint32_t s, bool insite, uint32_t end_t, uint32_t end_n)
 {
     uint32_t ot = 0, ot1 = 0, on = 0, on1 = 0, refc = 'N';
     if (insite) {
@@ -1725,53 +1715,79 @@ __device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 
     const bool acgt = ref16 == 1u || ref16 == 2u || ref16 == 4u || ref16 == 8u;
     const bool cand = small && !done && acgt;
     if (__ballot(cand)) {
-        /* one count pass over both samples when every site fits the joint
-         * layout (the tumor's reads, padded to 4, then the normal's: <= 128
-         * elements, one 128-bit element set), else one pass per sample (as
-         * ln_block's separate mode) with a set each */
         const uint32_t nt4 = (nt + 3u) & ~3u;
-        const bool joint = !__ballot(cand && nt4 + nn > LN_N);
-        const uint32_t oa = cand ? ot : 0u, ob = cand ? on : 0u;
-        uint32_t cnt_T = 0, cnt_N = 0, c24_T = 0, c24_N = 0;
-        /* chunks with an off-reference read, kept in the wave's record rows
-         * (free until ln_block): words in capture[slot][lane], element flags
-         * in fl_all (4 bits per slot), the sample in smp_all */
-        uint4 *capture = reinterpret_cast<uint4 *>(&L.rec[0][0]);
-        static_assert(sizeof(L.rec) >= SS_NEAR_SLOTS * 64 * sizeof(uint4), "capture slots fit the record rows");
-        uint32_t nfl = 0, fl_all = 0, smp_all = 0;
-        const uint32_t *p0a = a.reads_t + oa, *p0b = a.reads_n + ob - (cand ? nt4 : 0u), *p1 = a.reads_n + ob;
-        for (uint32_t pass = 0; pass < (joint ? 1u : 2u); ++pass) {
-            const bool nrm = pass == 1u;
-            LaneIn in;
-            in.na = cand ? (nrm ? nn : nt) : 0u;
-            in.na4 = (in.na + 3u) & ~3u;
-            in.nb = joint && cand ? nn : 0u;
-            in.nca = in.na4 >> 2;
-            asm("" : "+v"(in.nca));
-            in.nab = in.na4 + in.nb;
-            in.pa = nrm ? p1 : p0a;
-            in.pb = joint ? p0b : in.pa;               /* a pass of one sample: chunks past its reads load the next sites' */
-            in.la = ln_lut_row(1u + (nrm ? 16u : 0u) + ref16);
-            in.lb = ln_lut_row(17u + ref16);
-            const uint32_t nch = wave_max((in.nab + 3u) >> 2);
-            /* as in ln_block: word loads when an x4 load could pass the end of the reads */
-            const uint32_t oo = nrm ? ob : oa, eo = nrm ? end_n : end_t;
-            in.tail = ln_uniform(__ballot(joint ? ((uint64_t)oa + in.na4 > (uint64_t)end_t ||
-                                                   (uint64_t)ob + 4u * nch > (uint64_t)end_n + in.na4)
-                                                : (uint64_t)oo + 4u * nch > (uint64_t)eo) ||
-                                 end_t < 4u || end_n < 4u);
-            uint32_t cnt_a = 0, cnt_t = 0, c24 = 0;
-            if (in.tail) ln_count_pass<2>(in, lut, nch, nrm ? 1u : 0u, cnt_a, cnt_t, c24, capture, lane, nfl, fl_all, smp_all);
-            else ln_count_pass<1>(in, lut, nch, nrm ? 1u : 0u, cnt_a, cnt_t, c24, capture, lane, nfl, fl_all, smp_all);
-            if (!nrm) {
-                cnt_T = cnt_a;
-                cnt_N = cnt_t - cnt_a;                 /* joint: the rest */
-                c24_T = c24 & 0xffffu;
-                c24_N = c24 >> 16;
-            } else {
-                cnt_N = cnt_a;
-                c24_N = c24 & 0xffffu;
+        /* word loads when a site's x4 loads could pass the end of the batch's reads */
+        const uint32_t tm = ln_uniform(__ballot(cand && ((uint64_t)ot + nt4 > end_t ||
+                                                         (uint64_t)on + ((nn + 3u) & ~3u) > end_n)) ||
+                                       end_t < 4u || end_n < 4u);
+        /* each round: TG lanes per site (group g = lane / TG takes site
+         * round * 64 / TG + g), the site's description by ds_bpermute */
+        const uint32_t j = lane & (TG - 1u);
+        const uint32_t pk = cand ? (nt | nn << 8 | ref16 << 16) : 0u;    /* nt, nn <= 128 */
+#pragma unroll 1
+        for (uint32_t r = 0; r < 64u / TG; ++r) {
+            const uint32_t site = r * (64u / TG) + lane / TG;
+            const int sa = (int)(site << 2);
+            const uint32_t g_pk = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)pk);
+            const uint32_t g_ot = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)ot);
+            const uint32_t g_on = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)on);
+            const uint32_t g_nt = g_pk & 0xffu, g_nn = (g_pk >> 8) & 0xffu, g_ref16 = (g_pk >> 16) & 0xfu;
+            const uint32_t g_nt4 = (g_nt + 3u) & ~3u;
+            const uint32_t g_nchk = g_pk ? (g_nt4 + g_nn + 3u) >> 2 : 0u;    /* the site's chunks (0: not a candidate) */
+            const uint32_t K = wave_max((g_nchk + TG - 1u) / TG);
+            if (K == 0u) continue;
+            const uint32_t la = ln_lut_row(1u + g_ref16), lb = ln_lut_row(17u + g_ref16);
+            const uint32_t *pt = a.reads_t + g_ot, *pn = a.reads_n + g_on - g_nt4;
+            uint32_t cnt_a = 0, cnt_t = 0, c24 = 0, gn = 0;
+#pragma unroll 1
+            for (uint32_t k = 0; k < K; ++k) {
+                const uint32_t c = k * TG + j;
+                const bool live = c < g_nchk;
+                const bool fa = 4u * c < g_nt4;
+                const uint32_t *src = (fa ? pt : pn) + 4u * c;
+                const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;
+                uint32_t x[4] = {0u, 0u, 0u, 0u};
+                if (tm) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (t < lim) x[t] = src[t];
+                } else if (live) {
+                    const u32x4_a4 q4 = *reinterpret_cast<const u32x4_a4 *>(src);
+                    x[0] = q4.x; x[1] = q4.y; x[2] = q4.z; x[3] = q4.w;
+                }
+                const uint32_t fl = tri_chunk(lut, x, lim, fa ? la : lb, fa, cnt_a, cnt_t, c24);
+                /* a chunk with an off-reference read: kept for its site, in
+                 * element order (slot = the group's earlier chunks) */
+                const uint64_t bal = __ballot(fl != 0u);
+                if (bal) {
+                    const uint32_t gb = (uint32_t)(bal >> (lane & ~(TG - 1u))) & ((1u << TG) - 1u);
+                    const uint32_t slot = gn + (uint32_t)__popc(gb & ((1u << j) - 1u));
+                    if (fl != 0u && slot < SS_NEAR_SLOTS) {
+                        T.cap[site][slot] = make_uint4(x[0], x[1], x[2], x[3]);
+                        reinterpret_cast<uint8_t *>(&T.capf[site])[slot] = (uint8_t)(fl | (fa ? 0u : 16u));
+                    }
+                    gn += (uint32_t)__popc(gb);
+                }
             }
+            cnt_a = tri_gsum(cnt_a);
+            cnt_t = tri_gsum(cnt_t);
+            c24 = tri_gsum(c24);
+            if (j == 0u) {
+                T.cnt_t[site] = cnt_a;
+                T.cnt_n[site] = cnt_t - cnt_a;
+                T.c24[site] = c24;
+                T.nfl[site] = gn;
+            }
+        }
+        wave_sync();
+        /* lane = site again */
+        uint32_t cnt_T = 0, cnt_N = 0, c24s = 0, nflc = 0, cf = 0;
+        if (cand) {
+            cnt_T = T.cnt_t[lane];
+            cnt_N = T.cnt_n[lane];
+            c24s = T.c24[lane];
+            nflc = T.nfl[lane];
+            cf = T.capf[lane];
         }
         const uint32_t r = (uint32_t)__builtin_ctz(ref16 | 16u);     /* the reference base (0..3 for cand) */
         uint32_t ca[4], cb[4];
@@ -1782,21 +1798,29 @@ __device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 
         }
         const uint32_t ma = ca[0] + ca[1] + ca[2] + ca[3] - ln_sel4(ca, r);
         const uint32_t mb = cb[0] + cb[1] + cb[2] + cb[3] - ln_sel4(cb, r);
-        const bool ok = cand && ma <= SS_NEAR_K && mb <= SS_NEAR_K;
+        /* the captured slots' flags (4 bits per slot) and samples */
+        const uint32_t nv = min(nflc, SS_NEAR_SLOTS);
+        uint32_t fl_all = (cf & 0xfu) | ((cf >> 8) & 0xfu) << 4 | ((cf >> 16) & 0xfu) << 8 | ((cf >> 24) & 0xfu) << 12;
+        const uint32_t smp_all = ((cf >> 4) & 1u) | ((cf >> 12) & 1u) << 1 | ((cf >> 20) & 1u) << 2 | ((cf >> 28) & 1u) << 3;
+        fl_all &= (1u << (4u * nv)) - 1u;
+        /* every off-reference read captured: a site past SS_NEAR_SLOTS flagged
+         * chunks lost some (and may not take the exit) */
+        const bool ok = cand && ma <= SS_NEAR_K && mb <= SS_NEAR_K && (uint32_t)__popc(fl_all) == ma + mb;
         if (__ballot(ok)) {
             /* the off-reference reads from the captured chunks, in element
              * order (the tumor's first); at most 2 SS_NEAR_K of them matter */
             if (!ok) fl_all = 0u;
             uint32_t key[2 * SS_NEAR_K];
-            const uint32_t *cw = reinterpret_cast<const uint32_t *>(capture);
+            const uint32_t *cw = reinterpret_cast<const uint32_t *>(&T.cap[lane][0]);
+            const uint32_t la = ln_lut_row(1u + ref16), lb = ln_lut_row(17u + ref16);
 #pragma unroll
             for (uint32_t i = 0; i < 2u * SS_NEAR_K; ++i) {
                 const bool has = fl_all != 0u;
-                const uint32_t bpos = ln_ffbl(fl_all) & 31u;
+                const uint32_t bpos = ln_ffbl(fl_all) & 15u;
                 fl_all &= fl_all - 1u;
                 const uint32_t slot = bpos >> 2;
-                const uint32_t rd = has ? cw[(slot * 64u + lane) * 4u + (bpos & 3u)] : 0u;
-                const uint32_t row = ln_lut_row(((smp_all >> slot) & 1u ? 17u : 1u) + ref16);
+                const uint32_t rd = has ? cw[4u * slot + (bpos & 3u)] : 0u;
+                const uint32_t row = (smp_all >> slot) & 1u ? lb : la;
                 uint32_t minq;
                 asm("v_min_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_1"
                     : "=v"(minq) : "v"(rd));
@@ -1810,25 +1834,78 @@ __device__ __forceinline__ bool ln_classify(const ss_score_args &a, const uint2 
 #pragma unroll
             for (uint32_t i = 0; i < SS_NEAR_K; ++i) {
                 kt[i] = i < ma ? key[i] : 0u;
-                const uint32_t j = ma + i;                   /* <= 2K - 1 */
-                const uint32_t kj = j == 0u ? key[0] : j == 1u ? key[1] : j == 2u ? key[2] : j == 3u ? key[3]
-                                  : j == 4u ? key[4] : key[5];
+                const uint32_t jj = ma + i;                  /* <= 2K - 1 */
+                const uint32_t kj = jj == 0u ? key[0] : jj == 1u ? key[1] : jj == 2u ? key[2] : jj == 3u ? key[3]
+                                  : jj == 4u ? key[4] : key[5];
                 kn[i] = i < mb ? kj : 0u;
             }
             /* both samples on every lane (no divergent region; a lane that
              * is not ok has no keys and its answer is dropped) */
-            const bool okt = ln_near_sample(kt, ca, c24_T, r, a.m, fk);
-            const bool okn = ln_near_sample(kn, cb, c24_N, r, a.m, fk);
+            const bool okt = ln_near_sample(kt, ca, c24s & 0xffffu, r, a.m, fk);
+            const bool okn = ln_near_sample(kn, cb, c24s >> 16, r, a.m, fk);
             done = done || (ok & okt & okn);
         }
+        wave_sync();                                     /* T is reused by the next block */
     }
     if (done) kernarg_args().score[s] = sc;
     return done;
 }
 
+/* Triage kernel (round 6): the early exit (tri_block) for every 64-site
+ * block of mean depth <= SS_EARLY_MAX_READS, lane = site; the sites it does
+ * not decide (and every site of a deeper block) are appended to the main
+ * kernel's list (one atomic per wave).  Launched only when no glf records are
+ * requested and the host's bound tables are valid (SS_MF_FAST); otherwise the
+ * main kernel scores every site itself.  Its own kernel because the exit path
+ * needs far fewer registers than the main kernel's 128-key network. */
+__global__ __launch_bounds__(SS_TRIAGE_BLOCK) __attribute__((amdgpu_waves_per_eu(SS_TRIAGE_WAVES_PER_EU)))
+void ss_score_triage(ss_score_args a)
+{
+    __shared__ double fk[LN_FK_ZERO + 1];
+    __shared__ uint2 lut[LN_LUT_BYTES / 8];
+    __shared__ TriLds TL[SS_TRIAGE_BLOCK / 64];
+    for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < LN_FK_LIVE ? ss_tab_fk(a.m)[i] : 0.0;
+    ln_lut_build(lut);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (SS_TRIAGE_BLOCK / 64);
+    const uint32_t n_sites = (uint32_t)a.n_sites;
+    const uint32_t nblocks = (n_sites + 63u) / 64u;
+    const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
+    /* a batch whose mean depth is well past the blocks' threshold lists every site */
+    const uint64_t all_reads = (uint64_t)(end_t - a.off_t[0]) + (end_n - a.off_n[0]);
+    const bool early = all_reads <= (uint64_t)(SS_EARLY_MAX_READS + 8u) * n_sites;
+    for (uint32_t blk = blockIdx.x * (SS_TRIAGE_BLOCK / 64) + wv; blk < nblocks; blk += nwaves) {
+        const uint32_t s = blk * 64u + lane;
+        const bool insite = s < n_sites;
+        /* the block's reads from its offsets (scalar loads) */
+        bool shallow = false;
+        if (early) {
+            const ss_score_args &k = kernarg_args();
+            const uint32_t s0 = blk * 64u, s1 = min(s0 + 64u, n_sites);
+            const uint32_t breads = (k.off_t[s1] - k.off_t[s0]) + (k.off_n[s1] - k.off_n[s0]);
+            shallow = breads <= SS_EARLY_MAX_READS * (s1 - s0);
+        }
+        bool need = insite;
+        if (shallow) need = insite && !tri_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n);
+        const uint64_t m = __ballot(need);
+        if (m) {
+            const ss_score_args &k = kernarg_args();
+            const uint32_t first = (uint32_t)__builtin_ctzll(m);
+            uint32_t base = 0;
+            if (lane == first) base = atomicAdd(k.tri_count, (uint32_t)__popcll(m));
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+            if (need) k.tri_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
+        }
+    }
+}
+
 /* compiled for 3 waves per SIMD: the per-lane network's 64 registers, the
  * chunk loads in flight and the key arithmetic need about 160 VGPRs (at 128
- * the compiler spills); the records take 8 KB of LDS per wave */
+ * the compiler spills); the records take 8 KB of LDS per wave.  Scores the
+ * triage kernel's list (a.tri_list) or, without one, every site. */
 __global__ __launch_bounds__(SS_MAIN_BLOCK) __attribute__((amdgpu_waves_per_eu(3)))
 void ss_score_main(ss_score_args a)
 {
@@ -1838,83 +1915,29 @@ void ss_score_main(ss_score_args a)
     /* qAddTable (somatic_sniper.c:13,101-107) in LDS as int16 (its entries lie
      * in [-512, 0]; 2 KB keeps 3 workgroups per CU within 160 KB) */
     __shared__ int16_t qtab[1024];
-    __shared__ uint16_t qq[LN_WAVES][128];          /* the early exit's queue: 63 carried + 64 new sites */
+    const uint32_t n_sites = (uint32_t)a.n_sites;
+    const bool listed = a.tri_list != nullptr;
+    const uint32_t n = listed ? min(*a.tri_count, n_sites) : n_sites;
+    const uint32_t nblocks = (n + 63u) / 64u;
+    const uint32_t nwaves = gridDim.x * LN_WAVES;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t gw = blockIdx.x * LN_WAVES + wv;
+    if (blockIdx.x * LN_WAVES >= nblocks) return;      /* no block for this workgroup (a short list) */
     for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < LN_FK_LIVE ? ss_tab_fk(a.m)[i] : 0.0;
     for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) qtab[i] = (int16_t)ss_tab_qadd(a.m)[i];
     ln_lut_build(lut);
     __syncthreads();
     const uint32_t lane = lane_id();
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     LaneLds &L = LL[wv];
-    const uint32_t nwaves = gridDim.x * LN_WAVES;
-    const uint32_t n_sites = (uint32_t)a.n_sites;
-    const uint32_t nblocks = (n_sites + 63u) / 64u;
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
-    const uint32_t gw = blockIdx.x * LN_WAVES + wv;
     uint32_t ndeep = 0;
-    /* the early exit (ln_classify) needs no glf output and the host's table;
-     * the sites it does not decide wait in the wave's queue (LDS entries
-     * k << 6 | lane: the wave's k-th block) and are scored 64 at a time by
-     * ln_block, so its lanes stay full */
-    /* a batch whose mean depth is well past the blocks' threshold (C4's 89
-     * reads per site) never looks at its blocks' depths */
-    const uint64_t all_reads = (uint64_t)(end_t - a.off_t[0]) + (end_n - a.off_n[0]);
-    const bool early = a.glf == nullptr && (a.m.flags & SS_MF_FAST) != 0u &&
-                       all_reads <= (uint64_t)(SS_EARLY_MAX_READS + 8u) * n_sites;
-    uint16_t *queue = qq[wv];
-    uint32_t qn = 0;                                          /* wave-uniform */
-    uint32_t k = 0, blk = gw;
-    /* one ln_block call site (three of them spilled): each iteration scores a
-     * block directly, or classifies a shallow one and scores a full queue
-     * batch, or at the end the queue's last, partial batch */
-    for (;;) {
-        uint32_t s = 0;
-        bool insite = false, run = true;
-        if (blk < nblocks) {
-            s = blk * 64u + lane;
-            insite = s < n_sites;
-            /* only shallow blocks take the exit: at 30x/30x it pays, at 60x/30x
-             * the count pass and the queued sites' second load cost more than
-             * the skipped work; the block's reads from its
-             * offsets (scalar loads) */
-            bool shallow = false;
-            if (early && k < 1024u) {                         /* (queue entries hold k < 1024) */
-                const uint32_t s0 = blk * 64u, s1 = min(s0 + 64u, n_sites);
-                const uint32_t breads = (a.off_t[s1] - a.off_t[s0]) + (a.off_n[s1] - a.off_n[s0]);
-                shallow = breads <= SS_EARLY_MAX_READS * (s1 - s0);
-            }
-            if (shallow) {
-                const bool need = insite && !ln_classify(kernarg_args(), lut, fk, L, lane, s, insite, end_t, end_n);
-                const uint64_t m = __ballot(need);
-                if (need)
-                    queue[qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-                        (uint16_t)(k << 6 | lane);
-                qn += (uint32_t)__popcll(m);
-                run = qn >= 64u;
-                if (run) {                                    /* a full batch of queued sites */
-                    qn -= 64u;
-                    wave_sync();
-                    const uint32_t e = queue[qn + lane];
-                    wave_sync();
-                    s = (gw + (e >> 6) * nwaves) * 64u + (e & 63u);
-                    insite = true;
-                }
-            }
-            blk += nwaves;
-            ++k;
-        } else if (qn) {                                      /* the wave's last, partial batch */
-            wave_sync();
-            const uint32_t e = lane < qn ? (uint32_t)queue[lane] : 0u;
-            wave_sync();
-            s = (gw + (e >> 6) * nwaves) * 64u + (e & 63u);
-            insite = lane < qn;
-            qn = 0;
-        } else {
-            break;
-        }
-        if (run) ln_block(kernarg_args(), s, insite, lut, fk, qtab, L, lane, gw, cap, end_t, end_n, ndeep);
+    for (uint32_t blk = gw; blk < nblocks; blk += nwaves) {
+        const uint32_t i = blk * 64u + lane;
+        const bool insite = i < n;
+        uint32_t s = i;
+        if (listed) s = insite ? kernarg_args().tri_list[i] : 0u;
+        ln_block(kernarg_args(), s, insite, lut, fk, qtab, L, lane, gw, cap, end_t, end_n, ndeep);
     }
     if (lane == 0 && ndeep) {
         /* one atomic numbers the segment and places its entries, so the
@@ -3140,11 +3163,15 @@ int ss_launch_tab_fingerprint(const uint8_t *tab, unsigned long long *out3, hipS
     return (int)hipGetLastError();
 }
 
-int ss_launch_score(const ss_score_args &a, int main_grid, int wide_grid, int deep_grid, int wild_grid,
-                    hipStream_t s, const hipEvent_t *ev)
+int ss_launch_score(const ss_score_args &a, int triage_grid, int main_grid, int wide_grid, int deep_grid,
+                    int wild_grid, hipStream_t s, const hipEvent_t *ev)
 {
     hipError_t e;
     if (ev) (void)hipEventRecord(ev[0], s);
+    if (a.tri_list) {
+        hipLaunchKernelGGL(ss_score_triage, dim3(triage_grid), dim3(SS_TRIAGE_BLOCK), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    }
     hipLaunchKernelGGL(ss_score_main, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[1], s);

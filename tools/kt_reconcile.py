@@ -4,7 +4,8 @@ SAME process (tools/r06_cfg.sh / r06_final_cfg.sh run the bench under
 `rocprofv3 --kernel-trace --stats`): the mean over the timed dispatches (the
 last `launches_timed` ones of the dominant kernel; the warmups' first,
 cold, dispatches excluded) against the HIP-event mean the bench printed, and
-the --stats average (all dispatches, warmups included) beside them.
+the --stats average (all dispatches, warmups included) beside them.  A kernel
+class 'a+b' (the triage and main kernels) is summed per launch.
     python3 tools/kt_reconcile.py <kt dir> <bench log of that run>"""
 import csv
 import json
@@ -22,14 +23,24 @@ def main(ktdir, log):
             trace = os.path.join(dp, "run_kernel_trace.csv")
         if "run_kernel_stats.csv" in fs:
             stats = os.path.join(dp, "run_kernel_stats.csv")
-    rows = sorted((int(x["Dispatch_Id"]), (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e6)
-                  for x in csv.DictReader(open(trace)) if x["Kernel_Name"].startswith(kern + "("))
+    # a kernel class ('ss_score_triage+ss_score_main'): its dispatches summed
+    # per launch, the last name closing a launch
+    names = kern.split("+")
+    disp = sorted((int(x["Dispatch_Id"]), x["Kernel_Name"].split("(")[0],
+                   (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e6)
+                  for x in csv.DictReader(open(trace)) if x["Kernel_Name"].split("(")[0] in names)
+    rows, acc = [], 0.0
+    for did, name, d in disp:
+        acc += d
+        if name == names[-1]:
+            rows.append((did, acc))
+            acc = 0.0
     n = r["launches_timed"]
     timed = [d for _, d in rows[-n:]]
     avg_stats = None
     for x in csv.DictReader(open(stats)):
-        if x["Name"].startswith(kern + "("):
-            avg_stats = float(x["AverageNs"]) / 1e6
+        if x["Name"].split("(")[0] in names:
+            avg_stats = (avg_stats or 0.0) + float(x["AverageNs"]) / 1e6
     out = {"kernel": kern, "dispatches": len(rows), "timed": n,
            "hip_events_ms": r["avg_kernel_ms"],
            "rocprof_timed_dispatches_ms": round(sum(timed) / len(timed), 4),
