@@ -1488,6 +1488,9 @@ __device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, boo
  * instruction touched 64 lines: the texture address and data units were busy
  * 83% / 94% of the kernel's cycles at C4) */
 #define TG 8u                        /* lanes per site in the count pass */
+#ifndef TRI_P
+#define TRI_P 4u                     /* chunk load instructions in flight per round */
+#endif
 #define SS_NEAR_SLOTS 4u             /* captured chunks per site: more means more than four off-reference reads */
 
 /* per wave: a round's per-site totals and the sites' captured chunks */
@@ -1739,22 +1742,37 @@ __device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *l
             const uint32_t la = ln_lut_row(1u + g_ref16), lb = ln_lut_row(17u + g_ref16);
             const uint32_t *pt = a.reads_t + g_ot, *pn = a.reads_n + g_on - g_nt4;
             uint32_t cnt_a = 0, cnt_t = 0, c24 = 0, gn = 0;
+            /* TRI_P chunk instructions of the round in flight together (one
+             * memory latency per TRI_P, not per chunk) */
 #pragma unroll 1
-            for (uint32_t k = 0; k < K; ++k) {
-                const uint32_t c = k * TG + j;
+            for (uint32_t kb = 0; kb < K; kb += TRI_P) {
+            uint32_t xb[TRI_P][4];
+#pragma unroll
+            for (uint32_t u = 0; u < TRI_P; ++u) {
+                const uint32_t c = (kb + u) * TG + j;
                 const bool live = c < g_nchk;
                 const bool fa = 4u * c < g_nt4;
                 const uint32_t *src = (fa ? pt : pn) + 4u * c;
                 const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;
-                uint32_t x[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) xb[u][t] = 0u;
                 if (tm) {
 #pragma unroll
                     for (int t = 0; t < 4; ++t)
-                        if (t < lim) x[t] = src[t];
+                        if (t < lim) xb[u][t] = src[t];
                 } else if (live) {
                     const u32x4_a4 q4 = *reinterpret_cast<const u32x4_a4 *>(src);
-                    x[0] = q4.x; x[1] = q4.y; x[2] = q4.z; x[3] = q4.w;
+                    xb[u][0] = q4.x; xb[u][1] = q4.y; xb[u][2] = q4.z; xb[u][3] = q4.w;
                 }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < TRI_P; ++u) {
+                if (kb + u >= K) break;                          /* wave-uniform */
+                const uint32_t c = (kb + u) * TG + j;
+                const bool live = c < g_nchk;
+                const bool fa = 4u * c < g_nt4;
+                const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;
+                const uint32_t (&x)[4] = xb[u];
                 const uint32_t fl = tri_chunk(lut, x, lim, fa ? la : lb, fa, cnt_a, cnt_t, c24);
                 /* a chunk with an off-reference read: kept for its site, in
                  * element order (slot = the group's earlier chunks) */
@@ -1768,6 +1786,7 @@ __device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *l
                     }
                     gn += (uint32_t)__popc(gb);
                 }
+            }
             }
             cnt_a = tri_gsum(cnt_a);
             cnt_t = tri_gsum(cnt_t);
@@ -1888,7 +1907,12 @@ void ss_score_triage(ss_score_args a)
             shallow = breads <= SS_EARLY_MAX_READS * (s1 - s0);
         }
         bool need = insite;
-        if (shallow) need = insite && !tri_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n);
+        if (shallow) {
+            /* every lane of the wave (tri_block's DPP / ballot / bpermute
+             * exchanges read all 64 lanes; it handles lanes past the batch) */
+            const bool d = tri_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n);
+            need = insite && !d;
+        }
         const uint64_t m = __ballot(need);
         if (m) {
             const ss_score_args &k = kernarg_args();
