@@ -362,6 +362,10 @@ def live_counters(args, kernel="ss_score_main"):
                                      (row["Counter_Name"], float(row["Counter_Value"]),
                                       float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))))
             dispatch_ns = {did: dns for _, did, (_, _, dns) in rows}
+            grbm = {}
+            for _, did, (cn, cv, _) in rows:
+                if cn == "GRBM_GUI_ACTIVE":
+                    grbm[did] = grbm.get(did, 0.0) + cv
             per = {}
             for gi, (ids, recs) in enumerate(_launch_groups(rows, names)):
                 d = per.setdefault(gi, {})
@@ -369,6 +373,10 @@ def live_counters(args, kernel="ss_score_main"):
                     d[cn] = d.get(cn, 0.0) + cv
                 # the launch's duration in this same profiled pass (ns): its dispatches' durations summed
                 d["_dur_ns"] = float(sum(dispatch_ns[i] for i in ids))
+                # the clock from the launch's longest dispatch (a short one's busy count
+                # includes its dispatch overhead beyond its own duration)
+                big = max(ids, key=lambda i: dispatch_ns[i])
+                d["_clock_pair"] = (grbm.get(big, 0.0), dispatch_ns[big])
             # one pass = one launch per batch; the first pass (cold tables) is dropped
             n_pass = len(per) // max(1, args.pmc_launches)
             ds = sorted(per)[n_pass:] or sorted(per)
@@ -376,8 +384,8 @@ def live_counters(args, kernel="ss_score_main"):
                 vals[c] = float(np.mean([per[k].get(c, 0.0) for k in ds]))
             if "GRBM_GUI_ACTIVE" in counters:
                 # busy cycles per XCD / duration, both of the same profiled dispatches
-                vals["_clock_ghz"] = float(np.mean([per[k]["GRBM_GUI_ACTIVE"] / 8.0 / per[k]["_dur_ns"]
-                                                    for k in ds if per[k].get("_dur_ns", 0) > 0]))
+                vals["_clock_ghz"] = float(np.mean([per[k]["_clock_pair"][0] / 8.0 / per[k]["_clock_pair"][1]
+                                                    for k in ds if per[k]["_clock_pair"][1] > 0]))
                 vals["_dur_ms_profiled"] = float(np.mean([per[k]["_dur_ns"] for k in ds])) / 1e6
             vals["_sites_per_launch"] = sites_per_launch(args)
         except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
@@ -880,7 +888,8 @@ def main():
                 "clock_ghz_profiled": round(pc["_clock_ghz"], 3) if pc.get("_clock_ghz") else None,
                 "kernel_ms_profiled": round(pc["_dur_ms_profiled"], 4) if pc.get("_dur_ms_profiled") else None,
                 "clock_source": "GRBM_GUI_ACTIVE / 8 over the same dispatches' durations in the same profiled "
-                                "pass (End - Start timestamps of rocprofv3's counter records)",
+                                "pass (End - Start timestamps of rocprofv3's counter records); of each launch's "
+                                "longest dispatch (the triage kernel when it runs)",
                 "source": "rocprofv3 --pmc, separate passes over a child scoring rank 0's own launches of this N: "
                           "per-launch means of the second pass",
             }
