@@ -79,8 +79,8 @@ struct ss_ctx {
     /* device memory (dev_alloc): blocks in use, blocks outgrown but possibly still read */
     std::vector<dev_blk> *blocks, *retired;
     uint64_t fp_expect[3];    /* host fingerprint of the uploaded tables: coef, lhet, the rest */
-    float near_esr[132];      /* SS_TAB_ESR (near_tables) */
-    float near_cmin[132];     /* SS_TAB_CMIN */
+    float near_esr[2052];     /* SS_TAB_ESR (near_tables) */
+    float near_cmin[260];     /* SS_TAB_CMIN */
     int fast_ok;              /* SS_MF_FAST */
     int counted;              /* included in g_live */
 };
@@ -287,34 +287,35 @@ static float round_down_f(double x)
     return f;
 }
 
-/* The bounds of the main kernel's early exit (ss_kernels.hip ln_classify,
- * DESIGN.md 4.1): for a sample whose reference-base group has c of its
- * contributing reads at minq >= 24, and tot contributing reads in all,
- *   esr[c]    <= esum[ref]:  24 (m[0] + .. + m[c - 1]) (1 - 1e-4), m[k] = min(fk[0 .. k]);
- *   cmin[tot] <= lh + coef[q][tot][k] over q in [4, 63], k in [1, tot] and
- *                lh = -4.343 lhet[..] (min with 0), less 0.01,
+/* The bounds of the early exit (ss_kernels.hip tri_block / trd_block,
+ * DESIGN.md 4.0): for a sample whose reference-base group has c of its
+ * contributing reads at minq >= 24, and tot contributing reads in all (after
+ * the rescale of sniper_maqcns.c:178-182, so tot <= 256),
+ *   esr[c]    <= esum[ref]:  24 (m[0] + .. + m[c - 1]) (1 - 2e-4), m[k] = min(fk[0 .. k]);
+ *   cmin[tot] <= lh + coef[q << 16 | tot << 8 | k] over q in [4, 63], k in [1, tot]
+ *                (the reference's index, OR and all: tot = 256 aliases into
+ *                the next q row's n = 0 entries, :195) and lh = -4.343 lhet[..]
+ *                (min with 0), less 0.01,
  * so every genotype without the reference base has p >= esr[c] + cmin[tot]
- * (its e sums esum[ref] and other non-negative esums, sniper_maqcns.c:184-210).
+ * (its e sums esum[ref] and other non-negative esums, :184-210).
  * The k-th q >= 24 read of the reference group's walk weighs fk[w] with w <= k
  * (w counts per strand), so its weight is >= m[k] whatever the shape of fk:
- * fk[n] = theta^n (1 - eta) + eta (sniper_maqcns.c:72) decreases for theta < 1
- * but increases for the theta > 1 that -T accepts (main.c:83 has no range
- * check), and then m[k] = fk[0].  The 1e-4 margin covers the float
- * accumulation of esum (<= 128 roundings of 2^-24 relative each), the 0.01
- * the float rounding of p; both tables round down.  Enabled only with
- * q_r >= 1 and finite tables. */
-static int near_tables(const ss_host_model_t &hm, float esr[132], float cmin[132])
+ * fk[n] = theta^n (1 - eta) + eta (:72) decreases for theta < 1 but increases
+ * for the theta > 1 that -T accepts (main.c:83 has no range check), and then
+ * m[k] = fk[0] (w saturates at 255: fk[min(k, 255)]).  The 2e-4 margin covers
+ * the float accumulation of esum (<= SS_NEAR_MAXN roundings of 2^-24
+ * relative each: 1.2e-4), the 0.01 the float rounding of p; both tables
+ * round down.  Enabled only with q_r >= 1 and finite tables. */
+static int near_tables(const ss_host_model_t &hm, float esr[2052], float cmin[260])
 {
-    for (int i = 0; i < 132; ++i) {
-        esr[i] = 0.0f;
-        cmin[i] = -1e30f;
-    }
+    for (int i = 0; i < 2052; ++i) esr[i] = 0.0f;
+    for (int i = 0; i < 260; ++i) cmin[i] = -1e30f;
     if (hm.q_r_int < 1) return 0;
     double F = 0.0, run_min = hm.fk[0];
-    for (int k = 0; k < 128; ++k) {
-        run_min = std::min(run_min, hm.fk[k]);
+    for (int k = 0; k < (int)SS_NEAR_MAXN; ++k) {
+        run_min = std::min(run_min, hm.fk[k < 255 ? k : 255]);
         F += run_min;
-        esr[k + 1] = round_down_f(24.0 * F * (1.0 - 1e-4));
+        esr[k + 1] = round_down_f(24.0 * F * (1.0 - 2e-4));
     }
     double lh = 0.0;
     for (int i = 0; i < 65536; ++i) {
@@ -322,11 +323,12 @@ static int near_tables(const ss_host_model_t &hm, float esr[132], float cmin[132
         if (!std::isfinite(v)) return 0;
         lh = std::min(lh, v);
     }
-    for (int n = 1; n <= 128; ++n) {
+    for (int n = 1; n <= 256; ++n) {
         double cm = 1e300;
         for (int q = 4; q < 64; ++q)
             for (int k = 1; k <= n; ++k) {
-                const double v = hm.coef[(size_t)q << 16 | (size_t)n << 8 | (size_t)k];
+                const size_t idx = (size_t)q << 16 | (size_t)n << 8 | (size_t)k;
+                const double v = hm.coef[idx];
                 if (!std::isfinite(v)) return 0;
                 cm = std::min(cm, v);
             }
@@ -450,8 +452,8 @@ extern "C" int ss_ctx_create(const ss_params_t *p, int device, ss_ctx_t **out)
             {SS_TAB_PRIOR, c->hm.prior, 160 * sizeof(int32_t)},
             {SS_TAB_JPRIOR, c->hm.jprior, 1600 * sizeof(int32_t)},
             {SS_TAB_NT16, ss_nt16_table, 256},
-            {SS_TAB_ESR, c->near_esr, 132 * sizeof(float)},
-            {SS_TAB_CMIN, c->near_cmin, 132 * sizeof(float)},
+            {SS_TAB_ESR, c->near_esr, 2052 * sizeof(float)},
+            {SS_TAB_CMIN, c->near_cmin, 260 * sizeof(float)},
         };
         for (auto &pt : parts)
             if (hipMemcpyAsync(c->d_tab + pt.off, pt.src, pt.n, hipMemcpyHostToDevice, hs) != hipSuccess) {

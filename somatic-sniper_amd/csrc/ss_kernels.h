@@ -19,9 +19,10 @@
 #define SS_TAB_PRIOR  (SS_TAB_QADD + (size_t)1024 * 4)            /* i32 [16 * 10]   */
 #define SS_TAB_JPRIOR (SS_TAB_PRIOR + (size_t)160 * 4)            /* i32 [16*10*10]  */
 #define SS_TAB_NT16   (SS_TAB_JPRIOR + (size_t)1600 * 4)          /* u8  [256]       */
-#define SS_TAB_ESR    (SS_TAB_NT16 + (size_t)256)                 /* f32 [132]: the early exit's esum bound per c24 */
-#define SS_TAB_CMIN   (SS_TAB_ESR + (size_t)132 * 4)              /* f32 [132]: its coef + lh bound per depth */
-#define SS_TAB_BYTES  (SS_TAB_CMIN + (size_t)132 * 4)
+#define SS_NEAR_MAXN  2048u                                       /* reads per sample the early exit takes */
+#define SS_TAB_ESR    (SS_TAB_NT16 + (size_t)256)                 /* f32 [2052]: the early exit's esum bound per c24 */
+#define SS_TAB_CMIN   (SS_TAB_ESR + (size_t)2052 * 4)             /* f32 [260]: its coef + lh bound per (rescaled) depth */
+#define SS_TAB_BYTES  (SS_TAB_CMIN + (size_t)260 * 4)
 
 #define SS_MF_JOINT 1u
 #define SS_MF_LOH   2u

@@ -1566,6 +1566,9 @@ __device__ __forceinline__ float ln_sel4f(const float (&v)[4], uint32_t i)
     return i == 0u ? v[0] : i == 1u ? v[1] : i == 2u ? v[2] : v[3];
 }
 
+__device__ __forceinline__ bool ln_near_eval(const float (&es)[4], const float (&fs)[4], const uint32_t (&craw)[4],
+                                             uint32_t c24r, uint32_t r, const ss_dev_model &m);
+
 /* One sample of the early exit's near-reference test (see tri_block):
  * keys (descending after the sort) of its <= SS_NEAR_K non-reference
  * contributing reads, 0 = none; c its contributing reads per group (the
@@ -1609,7 +1612,29 @@ __device__ __forceinline__ bool ln_near_sample(uint32_t (&k)[SS_NEAR_K], const u
         }
         c24nr += key && minq >= 24u ? 1u : 0u;
     }
-    const uint32_t tot = c[0] + c[1] + c[2] + c[3];          /* <= 128: no rescale (:178-182) */
+    return ln_near_eval(es, fs, c, c24 - c24nr, r, m);
+}
+
+/* The genotype part of the near-reference test for one sample: es / fs the
+ * non-reference groups' chains (the reference group's entries 0, unused),
+ * craw its contributing reads per group, c24r the reference group's reads of
+ * minq >= 24.  True when sniper_glf2cns (sniper_maqcns.c:250-273) is proven
+ * to call the reference homozygote. */
+__device__ __forceinline__ bool ln_near_eval(const float (&es)[4], const float (&fs)[4], const uint32_t (&craw)[4],
+                                             uint32_t c24r, uint32_t r, const ss_dev_model &m)
+{
+    /* the counts' rescale (:178-182), as rescale_counts: tot <= 256 after it */
+    uint32_t c[4];
+    uint32_t tot = craw[0] + craw[1] + craw[2] + craw[3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = craw[j];
+    if (__ballot(tot > 255u)) {
+        if (tot > 255u) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c[j] = (uint32_t)(int)(254.0 * (double)craw[j] / (double)(int)tot + 0.5);
+            tot = c[0] + c[1] + c[2] + c[3];
+        }
+    }
     /* the genotypes with the reference base, as geno_p (:184-214): t = 3 the
      * homozygote, t < 3 the heterozygote with base x_t */
     float pv[4];
@@ -1640,7 +1665,7 @@ __device__ __forceinline__ bool ln_near_sample(uint32_t (&k)[SS_NEAR_K], const u
         cf[t] = ss_tab_coef(m)[icv[t]];
         lv[t] = ss_tab_lhet(m)[ilv[t]];
     }
-    const float esr = ss_tab_esr(m)[c24 - c24nr];
+    const float esr = ss_tab_esr(m)[c24r];
     const float cmn = ss_tab_cmin(m)[tot];
 #pragma unroll
     for (uint32_t t = 0; t < 4u; ++t) {
@@ -1661,8 +1686,10 @@ __device__ __forceinline__ bool ln_near_sample(uint32_t (&k)[SS_NEAR_K], const u
     const float lb = esr + cmn;
     const float phr = pv[3];
     const float min_p = min(min(phr, pv[0]), min(pv[1], pv[2]));
-    /* (bitwise: no short-circuit branches) */
-    bool ok = (esr > max(max(es[0], es[1]), max(es[2], es[3]))) & (lb - phr >= 3.0f) & (phr - min_p <= 250.0f);
+    /* (bitwise: no short-circuit branches); the reference group keeps a
+     * count after the rescale, so every genotype without it has tmp2 > 0 */
+    bool ok = (esr > max(max(es[0], es[1]), max(es[2], es[3]))) & (lb - phr >= 3.0f) & (phr - min_p <= 250.0f) &
+              (ln_sel4(c, r) > 0u);
     const int lhr = (int)((double)(phr - min_p) + 0.5);
 #pragma unroll
     for (uint32_t t = 0; t < 3u; ++t) {

@@ -411,7 +411,7 @@ def test_context_outlives_other_contexts(pkg):
 
 
 SS_TAB_NT16 = 34091904          # ss_kernels.h: coef 32 MiB, lhet, fk, qAdd, prior, jprior, then nt16
-SS_TAB_BYTES = 34093216          # + the early exit's bound tables SS_TAB_ESR, SS_TAB_CMIN (2 x 528 B, round 6)
+SS_TAB_BYTES = 34101408          # + the early exit's bound tables SS_TAB_ESR (2052 f32), SS_TAB_CMIN (260 f32), round 6
 
 
 @pytest.mark.gpu

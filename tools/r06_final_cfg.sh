@@ -8,6 +8,10 @@ TAG=${1:-r06final}
 O=$R/gpurun_out/$TAG
 mkdir -p "$O/c4"
 export TMPDIR=/tmp
+# a heartbeat under gpurun_out/ (the long bench steps print only at their end)
+(while true; do date >> "$O/heartbeat"; sleep 50; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 timeout -k 10 500 python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$O/c4/bench.json" 2> "$O/c4/bench.err" || exit 1
 tail -n 1 "$O/c4/bench.json" | cut -c1-300
 (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c4/kt" -o run -- \
