@@ -836,8 +836,9 @@ def main():
         "roofline": {
             "bound": "hbm",
             # the main class: the triage kernel (run when no glf records are
-            # requested) and the main kernel, summed per launch
-            "kernel": {"main": "ss_score_triage+ss_score_main", "wide": "ss_score_group",
+            # requested), the deep triage (blocks past 128 reads per sample) and the
+            # main kernel, summed per launch
+            "kernel": {"main": "ss_score_triage+ss_score_triage_deep+ss_score_main", "wide": "ss_score_group",
                        "deep": "ss_score_deep"}[dom],
             "achieved": round(achieved, 2) if achieved else None,
             "peak": HBM_PEAK_GBS,

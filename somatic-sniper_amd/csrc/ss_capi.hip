@@ -50,7 +50,8 @@ struct ss_ctx {
     /* model on the device */
     uint8_t *d_tab;           /* all tables, SS_TAB_* layout (ss_kernels.h) */
     /* work lists */
-    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [5] deep2 count, [6..7] listed
+    uint32_t *d_counters;     /* [2] err (sticky), [3] scratch n_calls, [4] the deep triage list's count,
+                                 [5] deep2 count, [6..7] listed
                                  entries | segments << 32, [8] the group kernel's chunk counter,
                                  [9] the deep kernel's chunk counter, [10] deep3 count,
                                  [11] the triage list's count,
@@ -513,9 +514,10 @@ extern "C" int ss_table_copy(const ss_ctx_t *c, double *fk, double *coef, double
     return SS_OK;
 }
 
-/* the deep list buffer holds four lists of deep_cap entries: the main
+/* the deep list buffer holds five lists of deep_cap entries: the main
  * kernel's per-wave segments (deep), the group kernel's overflow (deep2), the
- * deep kernel's (deep3) and the triage kernel's undecided sites (tri).
+ * deep kernel's (deep3), the triage kernels' undecided sites (tri) and the
+ * triage kernel's sites of deeper blocks (dtri).
  * Grown for a batch larger than any before (by at least half, so a run of
  * growing batches allocates O(log) times); the old list may still be read by
  * the context's previous launch, so it is retired, not reused, until
@@ -529,7 +531,7 @@ static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
     if (cap < n_sites) return SS_E_INVAL;
     dev_release(c, *(void **)&c->d_deep_list, false);
     c->deep_cap = 0;
-    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 4 * cap * sizeof(uint32_t), s)) return rc;
+    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 5 * cap * sizeof(uint32_t), s)) return rc;
     c->deep_cap = (uint32_t)cap;
     return SS_OK;
 }
@@ -589,7 +591,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     /* counters: deep2, listed segments and entries, the group and deep
      * kernels' next chunks, deep3, the triage list (err is sticky until
      * ss_ctx_check) */
-    HIPCHK(hipMemsetAsync(c->d_counters + 5, 0, 7 * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(c->d_counters + 4, 0, 8 * sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
     memset(&a, 0, sizeof(a));
@@ -624,6 +626,8 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     const bool triage = o->glf == nullptr && c->fast_ok;
     a.tri_list = triage ? c->d_deep_list + 3 * (size_t)c->deep_cap : nullptr;
     a.tri_count = c->d_counters + 11;
+    a.dtri_list = c->d_deep_list + 4 * (size_t)c->deep_cap;
+    a.dtri_count = c->d_counters + 4;
     a.err = c->d_counters + 2;
     a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;
@@ -651,7 +655,9 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     const uint64_t tri_wpb = SS_TRIAGE_BLOCK / 64;
     const int triage_grid = (int)std::min<uint64_t>((site_blocks + tri_wpb - 1) / tri_wpb,
                                                     (uint64_t)c->n_cu * SS_TRIAGE_GRID_PER_CU);
-    int e = ss_launch_score(a, triage_grid, (int)blocks, wide_grid, deep_grid, wild_grid, s, evs);
+    const int triage_deep_grid = (int)std::min<uint64_t>((site_blocks + 3) / 4,
+                                                         (uint64_t)c->n_cu * SS_TRIAGE_DEEP_GRID_PER_CU);
+    int e = ss_launch_score(a, triage_grid, triage_deep_grid, (int)blocks, wide_grid, deep_grid, wild_grid, s, evs);
     if (e != 0) return SS_E_HIP;
     HIPCHK(hipEventRecord(c->done, s));
     c->launched = 1;

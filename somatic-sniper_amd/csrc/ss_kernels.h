@@ -86,6 +86,8 @@ struct ss_score_args {
     uint32_t  *tri_list;      /* the triage kernel's undecided sites, scored by the main kernel (null:
                                  no triage, the main kernel scores every site) */
     uint32_t  *tri_count;
+    uint32_t  *dtri_list;     /* the triage kernel's sites of deeper blocks, for the deep triage kernel */
+    uint32_t  *dtri_count;
     uint32_t  *err;           /* sticky error bits, see SS_KERR_* */
     uint8_t   *grp_rec;       /* the group kernel's fold records: SS_GRP_REC_BYTES per wave */
     ss_dev_model m;
@@ -103,6 +105,8 @@ struct ss_score_args {
 #define SS_TRIAGE_WAVES_PER_EU 6
 #endif
 #define SS_TRIAGE_GRID_PER_CU 64 /* triage workgroups per CU (grid-strided 64-site blocks) */
+#define SS_TRIAGE_DEEP_BLOCK 256 /* the deep triage kernel: 4 waves (16 lanes per site) */
+#define SS_TRIAGE_DEEP_GRID_PER_CU 8
 #define SS_MAIN_SITES      64    /* sites per main-kernel wave block           */
 #define SS_MAIN_GRID_PER_CU 128  /* main-kernel workgroups per CU: 3 resident (166 VGPRs, 52.5 KB LDS each),
                                     the rest queued as short-lived waves (+5.5% over 16 per CU) */
@@ -123,8 +127,8 @@ struct ss_score_args {
 #define SS_GRP_REC_BYTES   (SS_GRP_REC_MAX + 2 * SS_GRP_REC_PAD)
 
 /* Launchers (return hipError_t as int). */
-int ss_launch_score(const ss_score_args &a, int triage_grid, int main_grid, int wide_grid, int deep_grid,
-                    int wild_grid, hipStream_t s,
+int ss_launch_score(const ss_score_args &a, int triage_grid, int triage_deep_grid, int main_grid, int wide_grid,
+                    int deep_grid, int wild_grid, hipStream_t s,
                     const hipEvent_t *ev /* 4 events (before main, after main, after wide, after deep + wild) or null */);
 /* out3 (zeroed by the caller): fingerprint sums of coef, lhet and the rest (ss_host.h) */
 int ss_launch_tab_fingerprint(const uint8_t *tab, unsigned long long *out3, hipStream_t s);

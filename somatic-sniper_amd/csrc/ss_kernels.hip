@@ -31,6 +31,8 @@
  * division and double sqrt are correctly rounded (sqrt re-checked with fma);
  * accumulation order equals the reference's descending-key order.
  */
+#include <cstdio>
+
 #include "ss_kernels.h"
 
 #define SENT 0xffffffffu
@@ -1665,7 +1667,7 @@ __device__ __forceinline__ bool ln_near_eval(const float (&es)[4], const float (
         cf[t] = ss_tab_coef(m)[icv[t]];
         lv[t] = ss_tab_lhet(m)[ilv[t]];
     }
-    const float esr = ss_tab_esr(m)[c24r];
+    const float esr = ss_tab_esr(m)[min(c24r, SS_NEAR_MAXN)];          /* (clamped: a lane that is not ok) */
     const float cmn = ss_tab_cmin(m)[tot];
 #pragma unroll
     for (uint32_t t = 0; t < 4u; ++t) {
@@ -1754,8 +1756,9 @@ __device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *l
          * round * 64 / TG + g), the site's description by ds_bpermute */
         const uint32_t j = lane & (TG - 1u);
         const uint32_t pk = cand ? (nt | nn << 8 | ref16 << 16) : 0u;    /* nt, nn <= 128 */
+        /* TG rounds of 64 / TG sites each */
 #pragma unroll 1
-        for (uint32_t r = 0; r < 64u / TG; ++r) {
+        for (uint32_t r = 0; r < TG; ++r) {
             const uint32_t site = r * (64u / TG) + lane / TG;
             const int sa = (int)(site << 2);
             const uint32_t g_pk = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)pk);
@@ -1919,15 +1922,12 @@ void ss_score_triage(ss_score_args a)
     const uint32_t n_sites = (uint32_t)a.n_sites;
     const uint32_t nblocks = (n_sites + 63u) / 64u;
     const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
-    /* a batch whose mean depth is well past the blocks' threshold lists every site */
-    const uint64_t all_reads = (uint64_t)(end_t - a.off_t[0]) + (end_n - a.off_n[0]);
-    const bool early = all_reads <= (uint64_t)(SS_EARLY_MAX_READS + 8u) * n_sites;
     for (uint32_t blk = blockIdx.x * (SS_TRIAGE_BLOCK / 64) + wv; blk < nblocks; blk += nwaves) {
         const uint32_t s = blk * 64u + lane;
         const bool insite = s < n_sites;
         /* the block's reads from its offsets (scalar loads) */
-        bool shallow = false;
-        if (early) {
+        bool shallow;
+        {
             const ss_score_args &k = kernarg_args();
             const uint32_t s0 = blk * 64u, s1 = min(s0 + 64u, n_sites);
             const uint32_t breads = (k.off_t[s1] - k.off_t[s0]) + (k.off_n[s1] - k.off_n[s0]);
@@ -1940,6 +1940,295 @@ void ss_score_triage(ss_score_args a)
             const bool d = tri_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n);
             need = insite && !d;
         }
+        /* a deeper block's sites: the deep triage's list; undecided sites of
+         * a shallow block: the main kernel's */
+        const uint64_t m = __ballot(need);
+        if (m) {
+            const ss_score_args &k = kernarg_args();
+            uint32_t *cnt = shallow ? k.tri_count : k.dtri_count;
+            uint32_t *lst = shallow ? k.tri_list : k.dtri_list;
+            const uint32_t first = (uint32_t)__builtin_ctzll(m);
+            uint32_t base = 0;
+            if (lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+            if (need) lst[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
+        }
+    }
+}
+
+/* --------------------------------------------------------------------------
+ * Deep triage (round 6): the early exit for sites with a sample of 129 ..
+ * SS_NEAR_MAXN reads (the triage kernel lists the sites of its deeper
+ * blocks for it).  The same test as tri_block with counts past 255 rescaled
+ * (sniper_maqcns.c:178-182) and up to SS_NEAR_KD off-reference reads per
+ * sample: 16 lanes per site, 16-bit group counts, the off-reference reads
+ * themselves kept in LDS (in element order, the tumor's first), and a
+ * 16-key network per sample for their chains.
+ * ------------------------------------------------------------------------ */
+#define TGD 16u                      /* lanes per site */
+#define SS_NEAR_KD 16u               /* off-reference contributing reads per sample the deep test evaluates */
+#define SS_NEAR_WORDS 32u            /* off-reference reads kept per site */
+
+struct TriLdsD {
+    uint32_t capw[64][SS_NEAR_WORDS + 1];    /* the site's off-reference reads, element order (+1: bank spread) */
+    uint32_t t02[64], t13[64], n02[64], n13[64]; /* contributing reads of bases 0 | 2 << 16, 1 | 3 << 16 */
+    uint32_t c24[64];                        /* contributing reads of minq >= 24: tumor | normal << 16 */
+    uint32_t nw[64];                         /* off-reference reads seen (past SS_NEAR_WORDS: some lost) */
+};
+
+/* sum over the 16 lanes of a DPP row */
+__device__ __forceinline__ uint32_t trd_gsum(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);    /* quad_perm [1,0,3,2] */
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);    /* quad_perm [2,3,0,1] */
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);   /* row_half_mirror */
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false);   /* row_mirror */
+    return v;
+}
+
+/* exclusive prefix sum over the 16 lanes of a DPP row */
+__device__ __forceinline__ uint32_t trd_xscan(uint32_t v)
+{
+    uint32_t x = v;
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   /* row_shr:1 */
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   /* row_shr:2 */
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   /* row_shr:4 */
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   /* row_shr:8 */
+    return x - v;
+}
+
+/* the deep test's key of an off-reference read: the key build's 16-bit key
+ * without the sample bit (so 0xffff is a pad), minq in 8 bits (5..12) */
+__device__ __forceinline__ uint32_t trd_key(const uint2 *lut, uint32_t rd, uint32_t row)
+{
+    const uint32_t minq = min(rd & 0xffu, (rd >> 8) & 0xffu);
+    const uint32_t ex = reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(lut) + (((rd >> 13) & 0xf8u) ^ row))->x;
+    return (ex & 0x7fffu) | minq << 5 | ((rd >> 13) & 6u) | min(rd & 0x3f00u, 1u);
+}
+
+/* One sample of the deep test: v its off-reference reads' keys in the lane
+ * network's layout (16 elements, pads 0xffff), nk their number (<=
+ * SS_NEAR_KD), c / c24 as ln_near_sample */
+__device__ __forceinline__ bool ln_near_sample16(uint32_t (&v)[8], uint32_t nk, const uint32_t (&c)[4], uint32_t c24,
+                                                 uint32_t r, const ss_dev_model &m, const double *fk)
+{
+    ln_levels<8, 2>(v);                                  /* ascending; the pads on top */
+    float es[4] = {0.0f, 0.0f, 0.0f, 0.0f}, fs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const char *fkb = reinterpret_cast<const char *>(fk);
+    uint64_t W = 0;                                      /* w per (group, strand): 8-bit fields */
+    uint32_t c24nr = 0;
+    const uint32_t nmax = wave_max(nk);
+    /* the chains in the reference's descending walk: key nk - 1 down to 0 */
+#pragma unroll
+    for (int e = 15; e >= 0; --e) {
+        if ((uint32_t)e >= nmax) continue;               /* wave-uniform */
+        const uint32_t key = ln_elem<8>(v, e);
+        const bool live = (uint32_t)e < nk;
+        const uint32_t x = (key >> 13) & 3u;
+        const uint32_t minq = (key >> 5) & 0xffu;
+        const uint32_t q = max(minq, (key & 1u) << 2);    /* sniper_maqcns.c:165 */
+        const uint32_t sh = 8u * (2u * x + ((key >> 3) & 1u));
+        const uint32_t w = (uint32_t)(W >> sh) & 0xffu;
+        W += live ? 1ull << sh : 0ull;
+        const double fv = *reinterpret_cast<const double *>(fkb + 8u * (live ? w : (uint32_t)LN_FK_ZERO));
+        const float e0 = ln_sel4f(es, x), f0 = ln_sel4f(fs, x);
+        const float e1 = (float)((double)e0 + fv * (double)q);
+        const float f1 = (float)((double)f0 + fv);
+#pragma unroll
+        for (uint32_t b = 0; b < 4u; ++b) {
+            es[b] = b == x ? e1 : es[b];
+            fs[b] = b == x ? f1 : fs[b];
+        }
+        c24nr += live && minq >= 24u ? 1u : 0u;
+    }
+    return ln_near_eval(es, fs, c, c24 - c24nr, r, m);
+}
+
+/* the deep triage's work for one block of up to 64 listed sites (lane =
+ * list entry); true when it wrote the site's score */
+__device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *lut, const double *fk, TriLdsD &T,
+                                          uint32_t lane, uint32_t s, bool insite, uint32_t end_t, uint32_t end_n)
+{
+    uint32_t ot = 0, ot1 = 0, on = 0, on1 = 0, refc = 'N';
+    if (insite) {
+        ot = a.off_t[s];
+        ot1 = a.off_t[s + 1];
+        on = a.off_n[s];
+        on1 = a.off_n[s + 1];
+        refc = a.ref[s];
+    }
+    const uint32_t ref16 = ss_tab_nt16(a.m)[refc];
+    const uint32_t nt = ot1 - ot, nn = on1 - on;
+    const bool small = insite && ot <= ot1 && ot1 <= end_t && on <= on1 && on1 <= end_n && nt <= SS_NEAR_MAXN &&
+                       nn <= SS_NEAR_MAXN;
+    bool done = false;
+    int32_t sc = 255;
+    if (small && (refc == 'N' || nt == 0u || nn == 0u)) {
+        done = true;
+        sc = -1;
+    } else if (small && ref16 == 15u) {
+        done = true;
+    }
+    const bool acgt = ref16 == 1u || ref16 == 2u || ref16 == 4u || ref16 == 8u;
+    const bool cand = small && !done && acgt;
+    if (__ballot(cand)) {
+        const uint32_t nt4 = (nt + 3u) & ~3u;
+        const uint32_t tm = ln_uniform(__ballot(cand && ((uint64_t)ot + nt4 > end_t ||
+                                                         (uint64_t)on + ((nn + 3u) & ~3u) > end_n)) ||
+                                       end_t < 4u || end_n < 4u);
+        const uint32_t j = lane & (TGD - 1u);
+        const uint32_t pk = cand ? (nt | nn << 12 | ref16 << 24) : 0u;   /* nt, nn <= 2048 */
+        /* TGD rounds of 64 / TGD sites each */
+#pragma unroll 1
+        for (uint32_t rr = 0; rr < TGD; ++rr) {
+            const uint32_t site = rr * (64u / TGD) + lane / TGD;
+            const int sa = (int)(site << 2);
+            const uint32_t g_pk = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)pk);
+            const uint32_t g_ot = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)ot);
+            const uint32_t g_on = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)on);
+            const uint32_t g_nt = g_pk & 0xfffu, g_nn = (g_pk >> 12) & 0xfffu, g_ref16 = (g_pk >> 24) & 0xfu;
+            const uint32_t g_nt4 = (g_nt + 3u) & ~3u;
+            const uint32_t g_nchk = g_pk ? (g_nt4 + g_nn + 3u) >> 2 : 0u;
+            const uint32_t K = wave_max((g_nchk + TGD - 1u) / TGD);
+            if (K == 0u) continue;
+            const uint32_t la = ln_lut_row(1u + g_ref16), lb = ln_lut_row(17u + g_ref16);
+            const uint32_t *pt = a.reads_t + g_ot, *pn = a.reads_n + g_on - g_nt4;
+            uint32_t t02 = 0, t13 = 0, n02 = 0, n13 = 0, c24 = 0, gw = 0;
+#pragma unroll 1
+            for (uint32_t kb = 0; kb < K; kb += TRI_P) {
+                uint32_t xb[TRI_P][4];
+#pragma unroll
+                for (uint32_t u = 0; u < TRI_P; ++u) {
+                    const uint32_t c = (kb + u) * TGD + j;
+                    const bool live = c < g_nchk;
+                    const bool fa = 4u * c < g_nt4;
+                    const uint32_t *src = (fa ? pt : pn) + 4u * c;
+                    const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) xb[u][t] = 0u;
+                    if (tm) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            if (t < lim) xb[u][t] = src[t];
+                    } else if (live) {
+                        const u32x4_a4 q4 = *reinterpret_cast<const u32x4_a4 *>(src);
+                        xb[u][0] = q4.x; xb[u][1] = q4.y; xb[u][2] = q4.z; xb[u][3] = q4.w;
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < TRI_P; ++u) {
+                    if (kb + u >= K) break;                      /* wave-uniform */
+                    const uint32_t c = (kb + u) * TGD + j;
+                    const bool live = c < g_nchk;
+                    const bool fa = 4u * c < g_nt4;
+                    const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;
+                    uint32_t ca8 = 0, ct8 = 0;
+                    const uint32_t fl = tri_chunk(lut, xb[u], lim, fa ? la : lb, fa, ca8, ct8, c24);
+                    /* the chunk's 8-bit counts (<= 4 each) into 16-bit fields */
+                    const uint32_t e02 = ct8 & 0x00ff00ffu, e13 = (ct8 >> 8) & 0x00ff00ffu;
+                    t02 += fa ? e02 : 0u;
+                    t13 += fa ? e13 : 0u;
+                    n02 += fa ? 0u : e02;
+                    n13 += fa ? 0u : e13;
+                    /* the off-reference reads themselves, in element order */
+                    if (__ballot(fl != 0u)) {
+                        const uint32_t nf = (uint32_t)__popc(fl);
+                        const uint32_t pre = gw + trd_xscan(nf);
+#pragma unroll
+                        for (uint32_t t = 0; t < 4u; ++t) {
+                            const uint32_t idx = pre + (uint32_t)__popc(fl & ((1u << t) - 1u));
+                            if (((fl >> t) & 1u) && idx < SS_NEAR_WORDS) T.capw[site][idx] = xb[u][t];
+                        }
+                        gw += trd_gsum(nf);
+                    }
+                }
+            }
+            t02 = trd_gsum(t02);
+            t13 = trd_gsum(t13);
+            n02 = trd_gsum(n02);
+            n13 = trd_gsum(n13);
+            c24 = trd_gsum(c24);
+            if (j == 0u) {
+                T.t02[site] = t02;
+                T.t13[site] = t13;
+                T.n02[site] = n02;
+                T.n13[site] = n13;
+                T.c24[site] = c24;
+                T.nw[site] = gw;
+            }
+        }
+        wave_sync();
+        /* lane = site again */
+        uint32_t ca[4] = {0u, 0u, 0u, 0u}, cb[4] = {0u, 0u, 0u, 0u}, c24s = 0, nwc = 0;
+        if (cand) {
+            const uint32_t a02 = T.t02[lane], a13 = T.t13[lane], b02 = T.n02[lane], b13 = T.n13[lane];
+            ca[0] = a02 & 0xffffu; ca[1] = a13 & 0xffffu; ca[2] = a02 >> 16; ca[3] = a13 >> 16;
+            cb[0] = b02 & 0xffffu; cb[1] = b13 & 0xffffu; cb[2] = b02 >> 16; cb[3] = b13 >> 16;
+            c24s = T.c24[lane];
+            nwc = T.nw[lane];
+        }
+        const uint32_t r = (uint32_t)__builtin_ctz(ref16 | 16u);
+        const uint32_t ma = ca[0] + ca[1] + ca[2] + ca[3] - ln_sel4(ca, r);
+        const uint32_t mb = cb[0] + cb[1] + cb[2] + cb[3] - ln_sel4(cb, r);
+        const bool ok = cand && ma <= SS_NEAR_KD && mb <= SS_NEAR_KD && nwc == ma + mb;
+        if (__ballot(ok)) {
+            const uint32_t la = ln_lut_row(1u + ref16), lb = ln_lut_row(17u + ref16);
+            const uint32_t nka = ok ? ma : 0u, nkb = ok ? mb : 0u;
+            const uint32_t kmax = wave_max(max(nka, nkb));
+            uint32_t vt[8], vn[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) vt[i] = vn[i] = 0x0000ffffu;    /* pads: lo 0xffff, hi ~0xffff */
+#pragma unroll
+            for (uint32_t i = 0; i < SS_NEAR_KD; ++i) {
+                if (i >= kmax) break;                            /* wave-uniform */
+                const uint32_t kt = i < nka ? trd_key(lut, T.capw[lane][i], la) : 0xffffu;
+                const uint32_t kn = i < nkb ? trd_key(lut, T.capw[lane][nka + i], lb) : 0xffffu;
+                if (i < 8u) {
+                    vt[i] = (vt[i] & 0xffff0000u) | kt;
+                    vn[i] = (vn[i] & 0xffff0000u) | kn;
+                } else {
+                    vt[15 - i] = (vt[15 - i] & 0x0000ffffu) | (kt ^ 0xffffu) << 16;
+                    vn[15 - i] = (vn[15 - i] & 0x0000ffffu) | (kn ^ 0xffffu) << 16;
+                }
+            }
+            /* both samples on every lane (a lane that is not ok has no keys
+             * and its answer is dropped) */
+            const bool okt = ln_near_sample16(vt, nka, ca, c24s & 0xffffu, r, a.m, fk);
+            const bool okn = ln_near_sample16(vn, nkb, cb, c24s >> 16, r, a.m, fk);
+            done = done || (ok & okt & okn);
+        }
+        wave_sync();                                     /* T is reused by the next block */
+    }
+    if (done) kernarg_args().score[s] = sc;
+    return done;
+}
+
+/* Deep triage kernel: the triage kernel's list of sites in blocks past
+ * SS_EARLY_MAX_READS mean reads (lane = entry); undecided sites go on to the
+ * main kernel's list. */
+__global__ __launch_bounds__(SS_TRIAGE_DEEP_BLOCK) void ss_score_triage_deep(ss_score_args a)
+{
+    __shared__ double fk[LN_FK_ZERO + 1];
+    __shared__ uint2 lut[LN_LUT_BYTES / 8];
+    __shared__ TriLdsD TL[SS_TRIAGE_DEEP_BLOCK / 64];
+    const uint32_t n_list = min(*a.dtri_count, (uint32_t)a.n_sites);
+    const uint32_t nblocks = (n_list + 63u) / 64u;
+    if (blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) >= nblocks) return;
+    for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < LN_FK_LIVE ? ss_tab_fk(a.m)[i] : 0.0;
+    ln_lut_build(lut);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (SS_TRIAGE_DEEP_BLOCK / 64);
+    const uint32_t n_sites = (uint32_t)a.n_sites;
+    const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
+    for (uint32_t blk = blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) + wv; blk < nblocks; blk += nwaves) {
+        const uint32_t i = blk * 64u + lane;
+        const bool insite = i < n_list;
+        const uint32_t s = insite ? kernarg_args().dtri_list[i] : 0u;
+        const bool d = trd_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n);
+        const bool need = insite && !d;
         const uint64_t m = __ballot(need);
         if (m) {
             const ss_score_args &k = kernarg_args();
@@ -3214,23 +3503,44 @@ int ss_launch_tab_fingerprint(const uint8_t *tab, unsigned long long *out3, hipS
     return (int)hipGetLastError();
 }
 
-int ss_launch_score(const ss_score_args &a, int triage_grid, int main_grid, int wide_grid, int deep_grid,
-                    int wild_grid, hipStream_t s, const hipEvent_t *ev)
+#ifdef SS_DEBUG_SYNC
+/* A/B builds only: wait for each kernel and name the one that failed */
+#define SS_DBG_SYNC(name)                                                                          \
+    do {                                                                                           \
+        hipError_t de = hipStreamSynchronize(s);                                                   \
+        if (de != hipSuccess) {                                                                    \
+            fprintf(stderr, "[sniper_amd debug] %s: %s\n", name, hipGetErrorString(de));           \
+            return (int)de;                                                                        \
+        }                                                                                          \
+    } while (0)
+#else
+#define SS_DBG_SYNC(name) do { } while (0)
+#endif
+
+int ss_launch_score(const ss_score_args &a, int triage_grid, int triage_deep_grid, int main_grid, int wide_grid,
+                    int deep_grid, int wild_grid, hipStream_t s, const hipEvent_t *ev)
 {
     hipError_t e;
     if (ev) (void)hipEventRecord(ev[0], s);
     if (a.tri_list) {
         hipLaunchKernelGGL(ss_score_triage, dim3(triage_grid), dim3(SS_TRIAGE_BLOCK), 0, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+        SS_DBG_SYNC("ss_score_triage");
+        hipLaunchKernelGGL(ss_score_triage_deep, dim3(triage_deep_grid), dim3(SS_TRIAGE_DEEP_BLOCK), 0, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+        SS_DBG_SYNC("ss_score_triage_deep");
     }
     hipLaunchKernelGGL(ss_score_main, dim3(main_grid), dim3(SS_MAIN_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    SS_DBG_SYNC("ss_score_main");
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(ss_score_group, dim3(wide_grid), dim3(SS_WIDE_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    SS_DBG_SYNC("ss_score_group");
     if (ev) (void)hipEventRecord(ev[2], s);
     hipLaunchKernelGGL(ss_score_deep, dim3(deep_grid), dim3(SS_DEEP_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    SS_DBG_SYNC("ss_score_deep");
     hipLaunchKernelGGL(ss_score_wild, dim3(wild_grid), dim3(SS_WILD_BLOCK), 0, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     if (ev) (void)hipEventRecord(ev[3], s);

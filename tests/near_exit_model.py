@@ -1,9 +1,11 @@
 """CPU restatement of the main kernel's early exit (ss_kernels.hip ln_classify /
 ln_near_sample) -- test infrastructure, not a product path.
 
-For a site of reference A/C/G/T with <= 128 reads per sample, the exit writes
+For a site of reference A/C/G/T with <= 2048 reads per sample, the exit writes
 255 (not a candidate, somatic_sniper.c:156) when in both samples
-  * at most NEAR_K contributing reads lie off the reference base's group;
+  * at most NEAR_K contributing reads lie off the reference base's group (the
+    kernels take 3 in blocks of <= 128 reads per sample, 16 past them: their
+    exits are a subset of this model's);
   * those reads' group chains (sniper_maqcns.c:162-172) give the four
     genotypes with the reference base exactly (:184-214), and a lower bound
     esr[c24] + cmin[tot] covers the six without it (ss_capi.hip near_tables);
@@ -14,7 +16,8 @@ same float / double operations, so the soundness test can score the sites the
 model exits with the oracle (tests/test_early_exit_bound.py)."""
 import numpy as np
 
-NEAR_K = 3
+NEAR_K = 16          # off-reference reads per sample (the deep test's; the shallow one takes 3)
+MAXN = 2048          # reads per sample
 NT4 = {1: 0, 2: 1, 4: 2, 8: 3}
 F32 = np.float32
 
@@ -27,21 +30,22 @@ def _round_down_f(x):
 
 
 def near_tables(fk, coef, lhet, q_r):
-    """ss_capi.hip near_tables: (esr[132], cmin[132]) float32, None when disabled."""
+    """ss_capi.hip near_tables: (esr[2052], cmin[260]) float32, None when disabled."""
     q_r_int = int(q_r + 0.5)
     if q_r_int < 1:
         return None
-    esr = np.zeros(132, np.float32)
-    cmin = np.full(132, -1e30, np.float32)
+    esr = np.zeros(2052, np.float32)
+    cmin = np.full(260, -1e30, np.float32)
     F, run_min = 0.0, fk[0]
-    for k in range(128):
-        run_min = min(run_min, fk[k])
+    for k in range(MAXN):
+        run_min = min(run_min, fk[min(k, 255)])
         F += run_min
-        esr[k + 1] = _round_down_f(24.0 * F * (1.0 - 1e-4))
+        esr[k + 1] = _round_down_f(24.0 * F * (1.0 - 2e-4))
     lh = min(0.0, float(np.min(-4.343 * lhet)))
-    c3 = coef.reshape(64, 256, 256)
-    for n in range(1, 129):
-        cm = float(np.min(c3[4:64, n, 1:n + 1]))
+    for n in range(1, 257):
+        # the reference's index, OR and all (n = 256 aliases into the next q row)
+        idx = [(q << 16) | (n << 8) | k for q in range(4, 64) for k in range(1, n + 1)]
+        cm = float(np.min(coef[idx]))
         cmin[n] = _round_down_f(cm + lh - 0.01)
     return esr, cmin
 
@@ -90,6 +94,9 @@ def _sample(reads, r, ref16, tabs, t):
         fs[x] = F32(float(fs[x]) + fv)
         if minq >= 24:
             c24nr += 1
+    if sum(c) > 255:                                    # the rescale of sniper_maqcns.c:178-182
+        t0 = sum(c)
+        c = [int(254.0 * cj / t0 + 0.5) for cj in c]
     tot = sum(c)
     pv = []
     for tt in range(4):
@@ -112,7 +119,7 @@ def _sample(reads, r, ref16, tabs, t):
     lb = F32(e_r + cmin[tot])
     phr = pv[3]
     min_p = min(phr, pv[0], pv[1], pv[2])
-    ok = e_r > max(es) and F32(lb - phr) >= 3 and F32(phr - min_p) <= 250
+    ok = e_r > max(es) and F32(lb - phr) >= 3 and F32(phr - min_p) <= 250 and c[r] > 0
     lhr = int(float(F32(phr - min_p)) + 0.5)
     for tt in range(3):
         d = F32(pv[tt] - min_p)
@@ -125,7 +132,7 @@ def near_exit(ref16, reads_t, reads_n, tabs, t):
     """True when the exit scores the site 255 through the near-reference test
     (ref16: the reference's nt16 code; 'N', empty samples and IUPAC
     references are decided before this test)."""
-    if tabs is None or ref16 not in NT4 or not (1 <= len(reads_t) <= 128 and 1 <= len(reads_n) <= 128):
+    if tabs is None or ref16 not in NT4 or not (1 <= len(reads_t) <= MAXN and 1 <= len(reads_n) <= MAXN):
         return False
     r = NT4[ref16]
     return bool(_sample(reads_t, r, ref16, tabs, t)) and bool(_sample(reads_n, r, ref16, tabs, t))

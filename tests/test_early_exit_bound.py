@@ -15,27 +15,29 @@ class -- under option sets that change the model tables, including theta > 1
 import numpy as np
 import pytest
 
-from near_exit_model import NEAR_K, near_exit, near_tables
+from near_exit_model import MAXN, NEAR_K, near_exit, near_tables
+
+NEAR_K_SHALLOW = 3          # off-reference reads per sample the shallow triage takes
 
 OPTS = [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-p", "-Q", "0"], ["-T", "1.2"]]
 REF16 = {"A": 1, "C": 2, "G": 4, "T": 8}
 
 
-def _pressing_sites(pkg, rng, n_sites):
+def _pressing_sites(pkg, rng, n_sites, nmax=128, mmax=NEAR_K_SHALLOW + 1, c24max=14):
     sites = []
     for _ in range(n_sites):
         refc = "ACGT"[rng.integers(4)]
         r = "ACGT".index(refc)
         smp = []
         for _s in range(2):
-            n = int(rng.integers(1, 129))
-            c24 = int(min(n, rng.integers(0, 14)))
+            n = int(rng.integers(1, nmax + 1))
+            c24 = int(min(n, rng.integers(0, c24max)))
             alt = bool(rng.integers(2))
             rest_bq = int(rng.choice([4, 4, 0, 7, 23, 130]))
             reads = [pkg.pack_read(60, 24, 1 << r, (i & 1) if alt else 0) for i in range(c24)]
             reads += [pkg.pack_read(60 if rest_bq else int(rng.integers(0, 60)), rest_bq, 1 << r,
                                     (i & 1) if alt else int(rng.integers(2))) for i in range(n - c24)]
-            m = int(rng.integers(0, NEAR_K + 2))          # sometimes one more than the exit takes
+            m = int(rng.integers(0, mmax + 1))           # sometimes one more than the exit takes
             for _j in range(m):
                 b = int(rng.integers(4))
                 nt16 = int(rng.choice([1 << b, 15, 5, 0])) if b != r else 15
@@ -43,7 +45,7 @@ def _pressing_sites(pkg, rng, n_sites):
                 mq = int(rng.choice([60, int(rng.integers(0, 256)), 2]))
                 reads.insert(int(rng.integers(len(reads) + 1)),
                              pkg.pack_read(mq, bq, nt16, int(rng.integers(2))))
-            smp.append(reads[:128])
+            smp.append(reads[:nmax])
         sites.append((refc, smp[0], smp[1]))
     return sites
 
@@ -74,6 +76,19 @@ def test_near_exit_sound_pressing(pkg, oracle, opts):
     rng = np.random.default_rng(20260 + len(opts))
     sites = _pressing_sites(pkg, rng, 2500)
     _check(pkg, oracle, o, sites, t, tabs, min_exits=150)
+
+
+@pytest.mark.parametrize("opts", [[], ["-T", "1.2"], ["-T", "0.9", "-N", "3", "-r", "0.01"]])
+def test_near_exit_sound_deep(pkg, oracle, opts):
+    """the deep triage's samples (129 .. 2048 reads: counts rescaled past
+    255, up to 16 off-reference reads per sample), pressed the same way"""
+    o = oracle.Oracle(oracle.opts_to_params(list(opts)))
+    t = o.tables()
+    tabs = near_tables(t["fk"], t["coef"], t["lhet"], t["q_r"])
+    rng = np.random.default_rng(777 + len(opts))
+    sites = _pressing_sites(pkg, rng, 400, nmax=700, mmax=NEAR_K + 1, c24max=80)
+    sites += _pressing_sites(pkg, rng, 40, nmax=MAXN, mmax=NEAR_K + 1, c24max=80)
+    _check(pkg, oracle, o, sites, t, tabs, min_exits=5)
 
 
 @pytest.mark.parametrize("opts", [[], ["-T", "1.2"]])

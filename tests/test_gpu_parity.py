@@ -505,6 +505,25 @@ def test_near_exit_parity(pkg, oracle, opts):
         assert_parity(pkg, oracle, b, opts)
 
 
+@pytest.mark.parametrize("opts", [[], ["-J"], ["-T", "0.9", "-N", "3", "-r", "0.01"], ["-T", "1.2"]])
+def test_near_exit_deep_parity(pkg, oracle, opts):
+    """The deep triage (samples of 129 .. 2048 reads, counts rescaled past 255,
+    up to 16 off-reference reads per sample) on deep sites
+    built to press its bounds (tests/test_early_exit_bound.py) and on
+    synthetic panels at default and 10x error rates, mixed with shallow
+    blocks: every output against the oracle, with and without glf."""
+    from test_early_exit_bound import _pressing_sites
+    rng = np.random.default_rng(9100 + len(opts))
+    sites = _pressing_sites(pkg, rng, 600, nmax=700, mmax=17, c24max=80)
+    sites += _pressing_sites(pkg, rng, 60, nmax=2048, mmax=17, c24max=80)
+    sites += _pressing_sites(pkg, rng, 640, nmax=128)
+    assert_parity(pkg, oracle, pkg.Batch.from_sites(sites), opts)
+    for lt, ln, kw in ((500, 500, {}), (300, 280, dict(p_error=0.03, p_somatic=0.02, p_germline=0.02)),
+                       (1200, 1000, {}), (150, 100, {})):
+        b = pkg.synth_batch_host(pkg.Synth.default(lt, ln, seed=31 + lt, **kw), 0, 1200)
+        assert_parity(pkg, oracle, b, opts)
+
+
 @pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"], ["-T", "1.2"]])
 def test_all_reference_sites_match_real_reference(pkg, tmp_path, opts):
     """all_reference_sites through the compiled reference on THIS machine vs
