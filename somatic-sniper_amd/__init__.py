@@ -247,6 +247,8 @@ def load_library():
     lib.ss_kernel_time_log_k.argtypes = [vp, C.c_int, vp, C.c_int]
     if hasattr(lib, "ss__test_poke_table"):         # test hook, not in the public header
         lib.ss__test_poke_table.argtypes = [vp, u64, C.c_int]
+    if hasattr(lib, "ss__test_route_counts"):       # test hook, not in the public header
+        lib.ss__test_route_counts.argtypes = [vp, C.POINTER(C.c_uint32)]
     if lib.ss_abi_version() != 1:
         raise RuntimeError("libsniper_amd.so ABI mismatch")
     _LIB = lib
@@ -396,6 +398,14 @@ class Context:
     def _poke_table(self, byte_offset: int, value: int):
         """Test hook: overwrite one byte of the device tables (ss_ctx_check must then fail)."""
         _check(self.lib.ss__test_poke_table(self.h, byte_offset, value), "ss__test_poke_table")
+
+    def _route_counts(self):
+        """Test hook: the latest launch's routing -- the deep triage's blocks,
+        the sites left to the main kernel, those it queued for the group and
+        the deep kernels."""
+        out = (C.c_uint32 * 4)()
+        _check(self.lib.ss__test_route_counts(self.h, out), "ss__test_route_counts")
+        return {"deep_triage_blocks": out[0], "main_sites": out[1], "group_sites": out[2], "deep_sites": out[3]}
 
     def set_kernel_timing(self, enable: bool):
         _check(self.lib.ss_set_kernel_timing(self.h, 1 if enable else 0), "ss_set_kernel_timing")

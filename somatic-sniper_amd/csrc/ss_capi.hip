@@ -746,6 +746,25 @@ extern "C" int ss__test_poke_table(ss_ctx_t *c, uint64_t byte_offset, int value)
     return SS_OK;
 }
 
+/* test hook (not in the public header): the latest launch's routing counts
+ * -- out[0] the deep triage's blocks, out[1] the sites the triage kernels
+ * left to the main kernel, out[2] the sites the main kernel queued for the
+ * group kernel, out[3] for the deep kernel (its two lists) */
+extern "C" int ss__test_route_counts(ss_ctx_t *c, uint32_t *out)
+{
+    uint32_t h[12];
+    if (!c || !out) return SS_E_INVAL;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->launched) HIPCHK(hipStreamWaitEvent(c->hstream, c->done, 0));
+    HIPCHK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, c->hstream));
+    HIPCHK(hipStreamSynchronize(c->hstream));
+    out[0] = h[4];
+    out[1] = h[11];
+    out[2] = h[6];
+    out[3] = h[5] + h[10];
+    return SS_OK;
+}
+
 /* ---------------------------------------------------------- host path ---- */
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 

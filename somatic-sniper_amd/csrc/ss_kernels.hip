@@ -61,6 +61,58 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
+/* List appends staged per wave in a register (lanes [0, n) of `held` hold
+ * the staged entries, n wave-uniform) and published 64 entries per atomic,
+ * the rest once per workgroup at its end (stage_wg_flush): returning atomics
+ * on one address serialise at about 11 ns each on MI355X
+ * (tools/atomic_probe.hip), so one per wave per 64-site block cost the
+ * triage kernel 0.19 ms per launch at 500x. */
+__device__ __forceinline__ void stage_push(uint32_t &held, uint32_t &n, bool need, uint32_t val, uint32_t *cnt,
+                                           uint32_t *lst, uint32_t lane)
+{
+    const uint64_t m = __ballot(need);
+    if (!m) return;
+    const uint32_t c = (uint32_t)__popcll(m);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    /* a permutation of the lanes: the entries to lanes n, n + 1, .. (mod 64)
+     * in lane order, every other lane after them */
+    const uint32_t rank = need ? below : c + (lane - below);
+    const uint32_t p = (uint32_t)__builtin_amdgcn_ds_permute((int)(((n + rank) & 63u) << 2), (int)val);
+    if (n + c < 64u) {
+        held = lane >= n && lane < n + c ? p : held;
+        n += c;
+    } else {
+        const uint32_t full = lane >= n ? p : held;
+        uint32_t base = 0;
+        if (lane == 0u) base = atomicAdd(cnt, 64u);
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        lst[base + lane] = full;
+        n = n + c - 64u;                                 /* lanes [0, n) received the rest */
+        held = p;
+    }
+}
+
+/* every wave's staged entries, one atomic for the workgroup; scratch: LDS of
+ * 2 + 64 * waves words no wave uses any more */
+__device__ __forceinline__ void stage_wg_flush(uint32_t held, uint32_t n, uint32_t *cnt, uint32_t *lst,
+                                               uint32_t *scratch, uint32_t lane)
+{
+    __syncthreads();
+    if (threadIdx.x == 0u) scratch[0] = 0u;
+    __syncthreads();
+    uint32_t off = 0;
+    if (lane == 0u && n != 0u) off = atomicAdd(&scratch[0], n);
+    off = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
+    if (lane < n) scratch[2u + off + lane] = held;
+    __syncthreads();
+    const uint32_t total = scratch[0];
+    if (total == 0u) return;                             /* workgroup-uniform */
+    if (threadIdx.x == 0u) scratch[1] = atomicAdd(cnt, total);
+    __syncthreads();
+    const uint32_t base = scratch[1];
+    for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) lst[base + i] = scratch[2u + i];
+}
+
 struct SlotRes {
     uint8_t  lk[12];
     uint32_t cns;
@@ -1508,8 +1560,9 @@ struct TriLds {
  * counts and its reads of minq >= 24 (lim: elements of the chunk that are
  * reads); returns the element flags of the contributing reads whose group is
  * not the reference base's (the lookup table's bit 31) */
+template <bool S1 = false>
 __device__ __forceinline__ uint32_t tri_chunk(const uint2 *lut, const uint32_t (&x)[4], int lim, uint32_t row, bool fa,
-                                              uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24)
+                                              uint32_t &cnt_a, uint32_t &cnt_t, uint32_t &c24, uint32_t *c24s1 = nullptr)
 {
     uint32_t valid, vl;
     asm("v_med3_i32 %0, %1, 0, 4" : "=v"(vl) : "v"(lim));
@@ -1527,16 +1580,18 @@ __device__ __forceinline__ uint32_t tri_chunk(const uint2 *lut, const uint32_t (
         const uint32_t off = __umul24(((rd >> 13) & 0xf8u) ^ row, ln_nz(minq[t] | (rd & 0x3f00u)));
         ent[t] = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(lut) + off);
     }
-    uint32_t cc = 0, q = 0, fl = 0;
+    uint32_t cc = 0, q = 0, q1 = 0, fl = 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         cc += ent[t].y;
         q += minq[t] >= 24u ? 1u : 0u;             /* minq >= 24: contributing */
+        if (S1) q1 += minq[t] >= 24u ? (x[t] >> 20) & 1u : 0u;   /* of them on strand 1 (masked: minq 0) */
         fl |= (ent[t].x >> 31) << t;
     }
     cnt_t += cc;
     cnt_a += fa ? cc : 0u;
     c24 += fa ? q : q << 16;
+    if (S1) *c24s1 += fa ? q1 : q1 << 16;
     return fl;
 }
 
@@ -1569,7 +1624,7 @@ __device__ __forceinline__ float ln_sel4f(const float (&v)[4], uint32_t i)
 }
 
 __device__ __forceinline__ bool ln_near_eval(const float (&es)[4], const float (&fs)[4], const uint32_t (&craw)[4],
-                                             uint32_t c24r, uint32_t r, const ss_dev_model &m);
+                                             float esr, uint32_t r, const ss_dev_model &m);
 
 /* One sample of the early exit's near-reference test (see tri_block):
  * keys (descending after the sort) of its <= SS_NEAR_K non-reference
@@ -1614,7 +1669,7 @@ __device__ __forceinline__ bool ln_near_sample(uint32_t (&k)[SS_NEAR_K], const u
         }
         c24nr += key && minq >= 24u ? 1u : 0u;
     }
-    return ln_near_eval(es, fs, c, c24 - c24nr, r, m);
+    return ln_near_eval(es, fs, c, ss_tab_esr(m)[min(c24 - c24nr, SS_NEAR_MAXN)], r, m);
 }
 
 /* The genotype part of the near-reference test for one sample: es / fs the
@@ -1623,7 +1678,7 @@ __device__ __forceinline__ bool ln_near_sample(uint32_t (&k)[SS_NEAR_K], const u
  * minq >= 24.  True when sniper_glf2cns (sniper_maqcns.c:250-273) is proven
  * to call the reference homozygote. */
 __device__ __forceinline__ bool ln_near_eval(const float (&es)[4], const float (&fs)[4], const uint32_t (&craw)[4],
-                                             uint32_t c24r, uint32_t r, const ss_dev_model &m)
+                                             float esr, uint32_t r, const ss_dev_model &m)
 {
     /* the counts' rescale (:178-182), as rescale_counts: tot <= 256 after it */
     uint32_t c[4];
@@ -1667,7 +1722,6 @@ __device__ __forceinline__ bool ln_near_eval(const float (&es)[4], const float (
         cf[t] = ss_tab_coef(m)[icv[t]];
         lv[t] = ss_tab_lhet(m)[ilv[t]];
     }
-    const float esr = ss_tab_esr(m)[min(c24r, SS_NEAR_MAXN)];          /* (clamped: a lane that is not ok) */
     const float cmn = ss_tab_cmin(m)[tot];
 #pragma unroll
     for (uint32_t t = 0; t < 4u; ++t) {
@@ -1902,11 +1956,12 @@ __device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *l
 
 /* Triage kernel (round 6): the early exit (tri_block) for every 64-site
  * block of mean depth <= SS_EARLY_MAX_READS, lane = site; the sites it does
- * not decide (and every site of a deeper block) are appended to the main
- * kernel's list (one atomic per wave).  Launched only when no glf records are
- * requested and the host's bound tables are valid (SS_MF_FAST); otherwise the
- * main kernel scores every site itself.  Its own kernel because the exit path
- * needs far fewer registers than the main kernel's 128-key network. */
+ * not decide are appended to the main kernel's list, the deeper blocks
+ * themselves to the deep triage's (both staged per wave, stage_push).
+ * Launched only when no glf records are requested and the host's bound
+ * tables are valid (SS_MF_FAST); otherwise the main kernel scores every site
+ * itself.  Its own kernel because the exit path needs far fewer registers
+ * than the main kernel's 128-key network. */
 __global__ __launch_bounds__(SS_TRIAGE_BLOCK) __attribute__((amdgpu_waves_per_eu(SS_TRIAGE_WAVES_PER_EU)))
 void ss_score_triage(ss_score_args a)
 {
@@ -1922,6 +1977,7 @@ void ss_score_triage(ss_score_args a)
     const uint32_t n_sites = (uint32_t)a.n_sites;
     const uint32_t nblocks = (n_sites + 63u) / 64u;
     const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
+    uint32_t nb = 0, hb = 0;
     for (uint32_t blk = blockIdx.x * (SS_TRIAGE_BLOCK / 64) + wv; blk < nblocks; blk += nwaves) {
         const uint32_t s = blk * 64u + lane;
         const bool insite = s < n_sites;
@@ -1933,47 +1989,53 @@ void ss_score_triage(ss_score_args a)
             const uint32_t breads = (k.off_t[s1] - k.off_t[s0]) + (k.off_n[s1] - k.off_n[s0]);
             shallow = breads <= SS_EARLY_MAX_READS * (s1 - s0);
         }
-        bool need = insite;
+        const ss_score_args &k = kernarg_args();
         if (shallow) {
             /* every lane of the wave (tri_block's DPP / ballot / bpermute
              * exchanges read all 64 lanes; it handles lanes past the batch) */
             const bool d = tri_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n);
-            need = insite && !d;
-        }
-        /* a deeper block's sites: the deep triage's list; undecided sites of
-         * a shallow block: the main kernel's */
-        const uint64_t m = __ballot(need);
-        if (m) {
-            const ss_score_args &k = kernarg_args();
-            uint32_t *cnt = shallow ? k.tri_count : k.dtri_count;
-            uint32_t *lst = shallow ? k.tri_list : k.dtri_list;
-            const uint32_t first = (uint32_t)__builtin_ctzll(m);
-            uint32_t base = 0;
-            if (lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(m));
-            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
-            if (need) lst[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
+            const bool need = insite && !d;
+            const uint64_t m = __ballot(need);
+            if (m) {                                     /* few at 30x .. 100x: one atomic per wave */
+                const uint32_t first = (uint32_t)__builtin_ctzll(m);
+                uint32_t base = 0;
+                if (lane == first) base = atomicAdd(k.tri_count, (uint32_t)__popcll(m));
+                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+                if (need) k.tri_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
+            }
+        } else {
+            stage_push(hb, nb, lane == 0u, blk, k.dtri_count, k.dtri_list, lane);
         }
     }
+    const ss_score_args &k = kernarg_args();
+    uint32_t *scratch = reinterpret_cast<uint32_t *>(&TL[0]);
+    static_assert(sizeof(TL) >= 4u * (2u + SS_TRIAGE_BLOCK), "flush scratch");
+    stage_wg_flush(hb, nb, k.dtri_count, k.dtri_list, scratch, lane);
 }
 
 /* --------------------------------------------------------------------------
  * Deep triage (round 6): the early exit for sites with a sample of 129 ..
- * SS_NEAR_MAXN reads (the triage kernel lists the sites of its deeper
- * blocks for it).  The same test as tri_block with counts past 255 rescaled
+ * SS_NEAR_MAXN reads (the triage kernel lists its deeper blocks for it).
+ * The same test as tri_block with counts past 255 rescaled
  * (sniper_maqcns.c:178-182) and up to SS_NEAR_KD off-reference reads per
- * sample: 16 lanes per site, 16-bit group counts, the off-reference reads
- * themselves kept in LDS (in element order, the tumor's first), and a
- * 16-key network per sample for their chains.
+ * sample: 16 lanes per site, TRD_P chunk loads in flight per lane, 16-bit
+ * group counts, the off-reference reads' 16-bit keys kept in LDS (in element
+ * order, the tumor's first), and a 16-key network per sample for their
+ * chains.
  * ------------------------------------------------------------------------ */
 #define TGD 16u                      /* lanes per site */
 #define SS_NEAR_KD 16u               /* off-reference contributing reads per sample the deep test evaluates */
 #define SS_NEAR_WORDS 32u            /* off-reference reads kept per site */
+#define TRD_P 8u                     /* chunk loads in flight per lane (16, or two batches of 8
+                                        in flight: 10% slower at 3 waves per SIMD) */
 
 struct TriLdsD {
-    uint32_t capw[64][SS_NEAR_WORDS + 1];    /* the site's off-reference reads, element order (+1: bank spread) */
+    uint16_t capk[64][SS_NEAR_WORDS + 2];    /* the keys (trd_key) of the site's off-reference reads, element
+                                                order (+2: an odd word stride) */
     uint32_t t02[64], t13[64], n02[64], n13[64]; /* contributing reads of bases 0 | 2 << 16, 1 | 3 << 16 */
     uint32_t c24[64];                        /* contributing reads of minq >= 24: tumor | normal << 16 */
+    uint32_t c24s1[64];                      /* of them on strand 1 */
     uint32_t nw[64];                         /* off-reference reads seen (past SS_NEAR_WORDS: some lost) */
 };
 
@@ -2011,13 +2073,13 @@ __device__ __forceinline__ uint32_t trd_key(const uint2 *lut, uint32_t rd, uint3
  * network's layout (16 elements, pads 0xffff), nk their number (<=
  * SS_NEAR_KD), c / c24 as ln_near_sample */
 __device__ __forceinline__ bool ln_near_sample16(uint32_t (&v)[8], uint32_t nk, const uint32_t (&c)[4], uint32_t c24,
-                                                 uint32_t r, const ss_dev_model &m, const double *fk)
+                                                 uint32_t c24s1, uint32_t r, const ss_dev_model &m, const double *fk)
 {
     ln_levels<8, 2>(v);                                  /* ascending; the pads on top */
     float es[4] = {0.0f, 0.0f, 0.0f, 0.0f}, fs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     const char *fkb = reinterpret_cast<const char *>(fk);
     uint64_t W = 0;                                      /* w per (group, strand): 8-bit fields */
-    uint32_t c24nr = 0;
+    uint32_t c24nr = 0, c24nr1 = 0;
     const uint32_t nmax = wave_max(nk);
     /* the chains in the reference's descending walk: key nk - 1 down to 0 */
 #pragma unroll
@@ -2041,8 +2103,15 @@ __device__ __forceinline__ bool ln_near_sample16(uint32_t (&v)[8], uint32_t nk, 
             fs[b] = b == x ? f1 : fs[b];
         }
         c24nr += live && minq >= 24u ? 1u : 0u;
+        c24nr1 += live && minq >= 24u ? (key >> 3) & 1u : 0u;
     }
-    return ln_near_eval(es, fs, c, c24 - c24nr, r, m);
+    /* the reference group's reads of minq >= 24 lead its two strand chains
+     * (their keys sort first within a group), so its esum is at least the
+     * sum of the two chains' bounds (ss_capi.hip near_tables: esr is rounded
+     * down with a 2e-4 margin that covers this float add) */
+    const uint32_t r1 = c24s1 - c24nr1, r0 = (c24 - c24nr) - r1;
+    const float *esr = ss_tab_esr(m);
+    return ln_near_eval(es, fs, c, esr[min(r0, SS_NEAR_MAXN)] + esr[min(r1, SS_NEAR_MAXN)], r, m);
 }
 
 /* the deep triage's work for one block of up to 64 listed sites (lane =
@@ -2094,78 +2163,88 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
             if (K == 0u) continue;
             const uint32_t la = ln_lut_row(1u + g_ref16), lb = ln_lut_row(17u + g_ref16);
             const uint32_t *pt = a.reads_t + g_ot, *pn = a.reads_n + g_on - g_nt4;
-            uint32_t t02 = 0, t13 = 0, n02 = 0, n13 = 0, c24 = 0, gw = 0;
-#pragma unroll 1
-            for (uint32_t kb = 0; kb < K; kb += TRI_P) {
-                uint32_t xb[TRI_P][4];
+            uint32_t t02 = 0, t13 = 0, n02 = 0, n13 = 0, c24 = 0, c24s1 = 0, gw = 0;
+            /* a batch of TRD_P chunk loads per lane (a macro: as a lambda taking
+             * the array by reference it cost 50 VGPRs), and its processing
+             * (the kernel is VALU-bound: its time follows the instructions of
+             * tri_chunk and the capture) */
+#define TRD_LOAD(XB, KB)                                                                        \
+    _Pragma("unroll") for (uint32_t u = 0; u < TRD_P; ++u) {                                    \
+        const uint32_t c = ((KB) + u) * TGD + j;                                                \
+        const bool live = c < g_nchk;                                                           \
+        const bool fa = 4u * c < g_nt4;                                                         \
+        const uint32_t *src = (fa ? pt : pn) + 4u * c;                                          \
+        const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;             \
+        _Pragma("unroll") for (int t = 0; t < 4; ++t) XB[u][t] = 0u;                            \
+        if (tm) {                                                                               \
+            _Pragma("unroll") for (int t = 0; t < 4; ++t) if (t < lim) XB[u][t] = src[t];       \
+        } else if (live) {                                                                      \
+            const u32x4_a4 q4 = *reinterpret_cast<const u32x4_a4 *>(src);                       \
+            XB[u][0] = q4.x; XB[u][1] = q4.y; XB[u][2] = q4.z; XB[u][3] = q4.w;                 \
+        }                                                                                       \
+    }
+            auto pr = [&](const uint32_t (&xb)[TRD_P][4], uint32_t kb) {
 #pragma unroll
-                for (uint32_t u = 0; u < TRI_P; ++u) {
-                    const uint32_t c = (kb + u) * TGD + j;
-                    const bool live = c < g_nchk;
-                    const bool fa = 4u * c < g_nt4;
-                    const uint32_t *src = (fa ? pt : pn) + 4u * c;
-                    const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) xb[u][t] = 0u;
-                    if (tm) {
-#pragma unroll
-                        for (int t = 0; t < 4; ++t)
-                            if (t < lim) xb[u][t] = src[t];
-                    } else if (live) {
-                        const u32x4_a4 q4 = *reinterpret_cast<const u32x4_a4 *>(src);
-                        xb[u][0] = q4.x; xb[u][1] = q4.y; xb[u][2] = q4.z; xb[u][3] = q4.w;
-                    }
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < TRI_P; ++u) {
+                for (uint32_t u = 0; u < TRD_P; ++u) {
                     if (kb + u >= K) break;                      /* wave-uniform */
                     const uint32_t c = (kb + u) * TGD + j;
                     const bool live = c < g_nchk;
                     const bool fa = 4u * c < g_nt4;
                     const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;
                     uint32_t ca8 = 0, ct8 = 0;
-                    const uint32_t fl = tri_chunk(lut, xb[u], lim, fa ? la : lb, fa, ca8, ct8, c24);
+                    const uint32_t fl = tri_chunk<true>(lut, xb[u], lim, fa ? la : lb, fa, ca8, ct8, c24, &c24s1);
                     /* the chunk's 8-bit counts (<= 4 each) into 16-bit fields */
                     const uint32_t e02 = ct8 & 0x00ff00ffu, e13 = (ct8 >> 8) & 0x00ff00ffu;
                     t02 += fa ? e02 : 0u;
                     t13 += fa ? e13 : 0u;
                     n02 += fa ? 0u : e02;
                     n13 += fa ? 0u : e13;
-                    /* the off-reference reads themselves, in element order */
+                    /* the off-reference reads' keys, in element order */
                     if (__ballot(fl != 0u)) {
                         const uint32_t nf = (uint32_t)__popc(fl);
                         const uint32_t pre = gw + trd_xscan(nf);
 #pragma unroll
                         for (uint32_t t = 0; t < 4u; ++t) {
                             const uint32_t idx = pre + (uint32_t)__popc(fl & ((1u << t) - 1u));
-                            if (((fl >> t) & 1u) && idx < SS_NEAR_WORDS) T.capw[site][idx] = xb[u][t];
+                            if (((fl >> t) & 1u) && idx < SS_NEAR_WORDS)
+                                T.capk[site][idx] = (uint16_t)trd_key(lut, xb[u][t], fa ? la : lb);
                         }
                         gw += trd_gsum(nf);
                     }
                 }
+            };
+#pragma unroll 1
+            for (uint32_t kb = 0; kb < K; kb += TRD_P) {
+                uint32_t xb[TRD_P][4];
+                TRD_LOAD(xb, kb)
+                pr(xb, kb);
             }
+#undef TRD_LOAD
             t02 = trd_gsum(t02);
             t13 = trd_gsum(t13);
             n02 = trd_gsum(n02);
             n13 = trd_gsum(n13);
             c24 = trd_gsum(c24);
+            c24s1 = trd_gsum(c24s1);
             if (j == 0u) {
                 T.t02[site] = t02;
                 T.t13[site] = t13;
                 T.n02[site] = n02;
                 T.n13[site] = n13;
                 T.c24[site] = c24;
+                T.c24s1[site] = c24s1;
                 T.nw[site] = gw;
             }
         }
         wave_sync();
         /* lane = site again */
-        uint32_t ca[4] = {0u, 0u, 0u, 0u}, cb[4] = {0u, 0u, 0u, 0u}, c24s = 0, nwc = 0;
+        uint32_t ca[4] = {0u, 0u, 0u, 0u}, cb[4] = {0u, 0u, 0u, 0u}, c24s = 0, c24s1 = 0, nwc = 0;
         if (cand) {
             const uint32_t a02 = T.t02[lane], a13 = T.t13[lane], b02 = T.n02[lane], b13 = T.n13[lane];
             ca[0] = a02 & 0xffffu; ca[1] = a13 & 0xffffu; ca[2] = a02 >> 16; ca[3] = a13 >> 16;
             cb[0] = b02 & 0xffffu; cb[1] = b13 & 0xffffu; cb[2] = b02 >> 16; cb[3] = b13 >> 16;
             c24s = T.c24[lane];
+            c24s1 = T.c24s1[lane];
             nwc = T.nw[lane];
         }
         const uint32_t r = (uint32_t)__builtin_ctz(ref16 | 16u);
@@ -2173,7 +2252,6 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
         const uint32_t mb = cb[0] + cb[1] + cb[2] + cb[3] - ln_sel4(cb, r);
         const bool ok = cand && ma <= SS_NEAR_KD && mb <= SS_NEAR_KD && nwc == ma + mb;
         if (__ballot(ok)) {
-            const uint32_t la = ln_lut_row(1u + ref16), lb = ln_lut_row(17u + ref16);
             const uint32_t nka = ok ? ma : 0u, nkb = ok ? mb : 0u;
             const uint32_t kmax = wave_max(max(nka, nkb));
             uint32_t vt[8], vn[8];
@@ -2182,8 +2260,8 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
 #pragma unroll
             for (uint32_t i = 0; i < SS_NEAR_KD; ++i) {
                 if (i >= kmax) break;                            /* wave-uniform */
-                const uint32_t kt = i < nka ? trd_key(lut, T.capw[lane][i], la) : 0xffffu;
-                const uint32_t kn = i < nkb ? trd_key(lut, T.capw[lane][nka + i], lb) : 0xffffu;
+                const uint32_t kt = i < nka ? (uint32_t)T.capk[lane][i] : 0xffffu;
+                const uint32_t kn = i < nkb ? (uint32_t)T.capk[lane][nka + i] : 0xffffu;
                 if (i < 8u) {
                     vt[i] = (vt[i] & 0xffff0000u) | kt;
                     vn[i] = (vn[i] & 0xffff0000u) | kn;
@@ -2194,8 +2272,8 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
             }
             /* both samples on every lane (a lane that is not ok has no keys
              * and its answer is dropped) */
-            const bool okt = ln_near_sample16(vt, nka, ca, c24s & 0xffffu, r, a.m, fk);
-            const bool okn = ln_near_sample16(vn, nkb, cb, c24s >> 16, r, a.m, fk);
+            const bool okt = ln_near_sample16(vt, nka, ca, c24s & 0xffffu, c24s1 & 0xffffu, r, a.m, fk);
+            const bool okn = ln_near_sample16(vn, nkb, cb, c24s >> 16, c24s1 >> 16, r, a.m, fk);
             done = done || (ok & okt & okn);
         }
         wave_sync();                                     /* T is reused by the next block */
@@ -2204,42 +2282,36 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
     return done;
 }
 
-/* Deep triage kernel: the triage kernel's list of sites in blocks past
- * SS_EARLY_MAX_READS mean reads (lane = entry); undecided sites go on to the
- * main kernel's list. */
+/* Deep triage kernel: the blocks the triage kernel found past
+ * SS_EARLY_MAX_READS mean reads (a wave per listed block, lane = site);
+ * undecided sites go on to the main kernel's list. */
 __global__ __launch_bounds__(SS_TRIAGE_DEEP_BLOCK) void ss_score_triage_deep(ss_score_args a)
 {
     __shared__ double fk[LN_FK_ZERO + 1];
     __shared__ uint2 lut[LN_LUT_BYTES / 8];
     __shared__ TriLdsD TL[SS_TRIAGE_DEEP_BLOCK / 64];
-    const uint32_t n_list = min(*a.dtri_count, (uint32_t)a.n_sites);
-    const uint32_t nblocks = (n_list + 63u) / 64u;
-    if (blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) >= nblocks) return;
+    const uint32_t n_sites = (uint32_t)a.n_sites;
+    const uint32_t nlisted = min(*a.dtri_count, (n_sites + 63u) / 64u);
+    if (blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) >= nlisted) return;
     for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < LN_FK_LIVE ? ss_tab_fk(a.m)[i] : 0.0;
     ln_lut_build(lut);
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (SS_TRIAGE_DEEP_BLOCK / 64);
-    const uint32_t n_sites = (uint32_t)a.n_sites;
     const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
-    for (uint32_t blk = blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) + wv; blk < nblocks; blk += nwaves) {
-        const uint32_t i = blk * 64u + lane;
-        const bool insite = i < n_list;
-        const uint32_t s = insite ? kernarg_args().dtri_list[i] : 0u;
-        const bool d = trd_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n);
-        const bool need = insite && !d;
-        const uint64_t m = __ballot(need);
-        if (m) {
-            const ss_score_args &k = kernarg_args();
-            const uint32_t first = (uint32_t)__builtin_ctzll(m);
-            uint32_t base = 0;
-            if (lane == first) base = atomicAdd(k.tri_count, (uint32_t)__popcll(m));
-            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
-            if (need) k.tri_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
-        }
+    uint32_t ns = 0, hs = 0;
+    for (uint32_t i = blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) + wv; i < nlisted; i += nwaves) {
+        const uint32_t blk = kernarg_args().dtri_list[i];
+        const uint32_t s = blk * 64u + lane;
+        const bool insite = s < n_sites;
+        const bool d = trd_block(kernarg_args(), lut, fk, TL[wv], lane, insite ? s : 0u, insite, end_t, end_n);
+        const ss_score_args &k = kernarg_args();
+        stage_push(hs, ns, insite && !d, s, k.tri_count, k.tri_list, lane);
     }
+    const ss_score_args &k = kernarg_args();
+    static_assert(sizeof(TL) >= 4u * (2u + SS_TRIAGE_DEEP_BLOCK), "flush scratch");
+    stage_wg_flush(hs, ns, k.tri_count, k.tri_list, reinterpret_cast<uint32_t *>(&TL[0]), lane);
 }
 
 /* compiled for 3 waves per SIMD: the per-lane network's 64 registers, the
@@ -2436,14 +2508,20 @@ __global__ __launch_bounds__(SS_WIDE_BLOCK) void ss_score_group(ss_score_args a)
     uint8_t *unit_of = L.unit_of[wv];
     const uint32_t cap = (uint32_t)a.m.cap_mapQ;
     const uint32_t end_t = a.off_t[a.n_sites], end_n = a.off_n[a.n_sites];
+    /* chunks of GB sites, fewer when the list is short: a few deep sites left
+     * by the triage (500x: about 1 in 10^4) then spread over that many waves
+     * instead of queueing in one (a 32-site chunk of 1000-read samples took
+     * one wave 0.2 ms) */
+    const uint32_t gsz = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)min((uint32_t)GB, max(1u, (total + gridDim.x * GP_WAVES - 1u) / (gridDim.x * GP_WAVES))));
     for (;;) {
         /* per chunk: the lane's LDS addresses are formed inside the loop */
         const uint32_t lane = lane_id_here();
         uint32_t ch = 0;
         if (lane == 0u) ch = atomicAdd(kernarg_args().wide_next, 1u);
-        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * GB;
+        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) * gsz;
         if (first >= total) break;
-        const uint32_t G = total - first < GB ? total - first : GB;
+        const uint32_t G = total - first < gsz ? total - first : gsz;
         /* the chunk's entries, lane k = entry k, into LDS */
         {
             const ss_score_args &k = kernarg_args();

@@ -8,7 +8,9 @@ For a site of reference A/C/G/T with <= 2048 reads per sample, the exit writes
     exits are a subset of this model's);
   * those reads' group chains (sniper_maqcns.c:162-172) give the four
     genotypes with the reference base exactly (:184-214), and a lower bound
-    esr[c24] + cmin[tot] covers the six without it (ss_capi.hip near_tables);
+    esr[c24] + cmin[tot] covers the six without it (ss_capi.hip near_tables;
+    the deep triage bounds the reference group's two strand chains apart,
+    esr[c24 on strand 0] + esr[c24 on strand 1]: per_strand);
   * the bounds put the reference homozygote first in sniper_glf2cns
     (:250-273), with the homozygote fix (:216-233) not firing.
 `near_tables` restates the host tables, `near_exit` the device test with the
@@ -55,12 +57,12 @@ def _bar_e(e, f):
     return 4 if be < 4 else (63 if be > 63 else be)
 
 
-def _sample(reads, r, ref16, tabs, t):
+def _sample(reads, r, ref16, tabs, t, per_strand=False):
     """one sample's test; None = the exit does not apply"""
     esr, cmin = tabs
     fk, coef, lhet, q_r_int = t["fk"], t["coef"], t["lhet"], int(t["q_r"] + 0.5)
     c = [0, 0, 0, 0]
-    c24 = 0
+    c24 = c24s1 = 0
     keys = []
     for x in reads:
         x = int(x)
@@ -74,6 +76,7 @@ def _sample(reads, r, ref16, tabs, t):
         c[base] += 1
         if minq >= 24:
             c24 += 1
+            c24s1 += st
         if base != r:
             keys.append(base << 13 | minq << 5 | hb << 4 | st << 3 | (bq >> 6) << 1 | (1 if bq & 0x3F else 0))
     if len(keys) > NEAR_K:
@@ -81,7 +84,7 @@ def _sample(reads, r, ref16, tabs, t):
     keys.sort(reverse=True)
     es, fs = [F32(0)] * 4, [F32(0)] * 4
     seen = {}
-    c24nr = 0
+    c24nr = c24nr1 = 0
     for key in keys:
         x = (key >> 13) & 3
         minq = (key >> 5) & 0xFF
@@ -94,6 +97,7 @@ def _sample(reads, r, ref16, tabs, t):
         fs[x] = F32(float(fs[x]) + fv)
         if minq >= 24:
             c24nr += 1
+            c24nr1 += (key >> 3) & 1
     if sum(c) > 255:                                    # the rescale of sniper_maqcns.c:178-182
         t0 = sum(c)
         c = [int(254.0 * cj / t0 + 0.5) for cj in c]
@@ -115,7 +119,11 @@ def _sample(reads, r, ref16, tabs, t):
             lh = -4.343 * float(lhet[c[j0] << 8 | c[k0]])
             v = F32((lh + float(e)) + cf) if c2 else F32(lh)
         pv.append(F32(0) if v < 0 else v)
-    e_r = esr[c24 - c24nr]
+    if per_strand:
+        r1 = c24s1 - c24nr1
+        e_r = F32(esr[c24 - c24nr - r1] + esr[r1])
+    else:
+        e_r = esr[c24 - c24nr]
     lb = F32(e_r + cmin[tot])
     phr = pv[3]
     min_p = min(phr, pv[0], pv[1], pv[2])
@@ -128,11 +136,13 @@ def _sample(reads, r, ref16, tabs, t):
     return ok
 
 
-def near_exit(ref16, reads_t, reads_n, tabs, t):
+def near_exit(ref16, reads_t, reads_n, tabs, t, per_strand=False):
     """True when the exit scores the site 255 through the near-reference test
     (ref16: the reference's nt16 code; 'N', empty samples and IUPAC
-    references are decided before this test)."""
+    references are decided before this test).  per_strand: the deep
+    triage's bound of the reference group's esum."""
     if tabs is None or ref16 not in NT4 or not (1 <= len(reads_t) <= MAXN and 1 <= len(reads_n) <= MAXN):
         return False
     r = NT4[ref16]
-    return bool(_sample(reads_t, r, ref16, tabs, t)) and bool(_sample(reads_n, r, ref16, tabs, t))
+    return (bool(_sample(reads_t, r, ref16, tabs, t, per_strand)) and
+            bool(_sample(reads_n, r, ref16, tabs, t, per_strand)))

@@ -54,8 +54,8 @@ def _ref16(rc):
     return REF16.get((rc if isinstance(rc, str) else chr(rc)).upper(), 15)
 
 
-def _check(pkg, oracle, o, sites, t, tabs, min_exits):
-    exits = np.array([near_exit(_ref16(rc), rt, rn, tabs, t) for rc, rt, rn in sites])
+def _check(pkg, oracle, o, sites, t, tabs, min_exits, per_strand=False):
+    exits = np.array([near_exit(_ref16(rc), rt, rn, tabs, t, per_strand) for rc, rt, rn in sites])
     batch = pkg.Batch.from_sites(sites)
     score, _, _ = o.score_batch(batch.ref, batch.off_tumor, batch.off_normal, batch.reads_tumor,
                                 batch.reads_normal, want_glf=False)
@@ -76,6 +76,9 @@ def test_near_exit_sound_pressing(pkg, oracle, opts):
     rng = np.random.default_rng(20260 + len(opts))
     sites = _pressing_sites(pkg, rng, 2500)
     _check(pkg, oracle, o, sites, t, tabs, min_exits=150)
+    # the deep triage's per-strand bound on the same sites (it takes every
+    # site of a block past 128 mean reads, shallow ones included)
+    _check(pkg, oracle, o, sites, t, tabs, min_exits=150, per_strand=True)
 
 
 @pytest.mark.parametrize("opts", [[], ["-T", "1.2"], ["-T", "0.9", "-N", "3", "-r", "0.01"]])
@@ -88,7 +91,7 @@ def test_near_exit_sound_deep(pkg, oracle, opts):
     rng = np.random.default_rng(777 + len(opts))
     sites = _pressing_sites(pkg, rng, 400, nmax=700, mmax=NEAR_K + 1, c24max=80)
     sites += _pressing_sites(pkg, rng, 40, nmax=MAXN, mmax=NEAR_K + 1, c24max=80)
-    _check(pkg, oracle, o, sites, t, tabs, min_exits=5)
+    _check(pkg, oracle, o, sites, t, tabs, min_exits=5, per_strand=True)
 
 
 @pytest.mark.parametrize("opts", [[], ["-T", "1.2"]])

@@ -524,6 +524,49 @@ def test_near_exit_deep_parity(pkg, oracle, opts):
         assert_parity(pkg, oracle, b, opts)
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_misaligned_read_arrays(pkg, oracle, shift):
+    """Device-resident read arrays that start 4, 8 or 12 bytes past a 16-byte
+    boundary (views into larger buffers): the kernels' 16-byte chunk loads
+    are then misaligned everywhere and the last site's last chunk ends within
+    three elements of the array's end.  Deep, shallow and mixed blocks, every
+    score against the oracle, with the routing through both triage kernels
+    checked."""
+    import torch
+    from test_early_exit_bound import _pressing_sites
+    rng = np.random.default_rng(4400 + shift)
+    sites = _pressing_sites(pkg, rng, 200, nmax=700, mmax=17, c24max=80)
+    sites += _pressing_sites(pkg, rng, 200, nmax=128)
+    b1 = pkg.synth_batch_host(pkg.Synth.default(500, 500, seed=77 + shift), 0, 256)
+    b2 = pkg.synth_batch_host(pkg.Synth.default(60, 30, seed=78 + shift), 0, 256)
+    sites += [b1.site(i) for i in range(b1.n_sites)] + [b2.site(i) for i in range(b2.n_sites)]
+    batch = pkg.Batch.from_sites(sites)
+    o = oracle.Oracle(oracle.opts_to_params([]))
+    o_score, _, _ = o.score_batch(batch.ref, batch.off_tumor, batch.off_normal, batch.reads_tumor,
+                                  batch.reads_normal, want_glf=False)
+    dev = torch.device("cuda", 0)
+
+    def shifted(x):
+        buf = torch.full((x.size + shift + 4,), 0xFFFFFFFF, dtype=torch.int64).to(torch.int32)
+        buf[shift:shift + x.size] = torch.from_numpy(x.view(np.int32))
+        return buf.to(dev)[shift:shift + x.size]
+
+    rt, rn = shifted(batch.reads_tumor), shifted(batch.reads_normal)
+    assert rt.data_ptr() % 16 == 4 * shift and rn.data_ptr() % 16 == 4 * shift
+    t = {k: torch.from_numpy(getattr(batch, k).view(np.int32) if getattr(batch, k).dtype == np.uint32
+                             else getattr(batch, k)).to(dev) for k in ("ref", "off_tumor", "off_normal")}
+    score = torch.empty(batch.n_sites, dtype=torch.int32, device=dev)
+    with pkg.Context(pkg.Params.default(), device=0) as ctx:
+        ctx.score_device(t["ref"], t["off_tumor"], t["off_normal"], rt, rn, score=score)
+        torch.cuda.synchronize(dev)
+        ctx.check()
+        route = ctx._route_counts()
+    got = score.cpu().numpy()
+    bad = np.nonzero(got != o_score)[0]
+    assert bad.size == 0, f"{bad.size} score mismatches, first {bad[:5]}: gpu {got[bad[:5]]} oracle {o_score[bad[:5]]}"
+    assert route["deep_triage_blocks"] > 0
+
+
 @pytest.mark.parametrize("opts", [[], ["-J"], ["-p", "-Q", "0"], ["-T", "1.2"]])
 def test_all_reference_sites_match_real_reference(pkg, tmp_path, opts):
     """all_reference_sites through the compiled reference on THIS machine vs

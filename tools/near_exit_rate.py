@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Fraction of synthetic sites the main kernel's early exit decides (the CPU
-model tests/near_exit_model.py, default options), per depth configuration.
+"""Fraction of synthetic sites the triage kernels' early exit decides (the CPU
+model tests/near_exit_model.py, default options), per depth configuration,
+with the single-chain and the per-strand (deep triage) esum bound.
     python3 tools/near_exit_rate.py [n_sites]"""
 import os
 import sys
@@ -21,9 +22,9 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 4000
 o = oracle.Oracle(oracle.opts_to_params([]))
 t = o.tables()
 tabs = near_tables(t["fk"], t["coef"], t["lhet"], t["q_r"])
-for lt, ln in ((30, 30), (60, 30), (100, 60)):
+for lt, ln in ((30, 30), (60, 30), (100, 60), (500, 500), (1200, 1000)):
     b = pkg.synth_batch_host(pkg.Synth.default(lt, ln), 0, n)
-    ex = 0
+    ex = exs = 0
     small = 0
     for i in range(b.n_sites):
         rc, rt, rn = b.site(i)
@@ -31,4 +32,6 @@ for lt, ln in ((30, 30), (60, 30), (100, 60)):
         if len(rt) <= 128 and len(rn) <= 128:
             small += 1
         ex += near_exit(r16, rt, rn, tabs, t)
-    print(f"{lt}x/{ln}x: {ex}/{b.n_sites} sites exit ({ex / b.n_sites:.3f}); <=128 reads per sample: {small}")
+        exs += near_exit(r16, rt, rn, tabs, t, per_strand=True)
+    print(f"{lt}x/{ln}x: {ex}/{b.n_sites} sites exit ({ex / b.n_sites:.3f}), per-strand bound {exs} "
+          f"({exs / b.n_sites:.3f}); <=128 reads per sample: {small}")
