@@ -2168,10 +2168,7 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
              * the array by reference it cost 50 VGPRs), and its processing
              * (the kernel is VALU-bound: its time follows the instructions of
              * tri_chunk and the capture) */
-#define TRD_LOAD(XB, KB)                                                                        \
-    _Pragma("unroll") for (uint32_t u = 0; u < TRD_P; ++u) {                                    \
-        const uint32_t c = ((KB) + u) * TGD + j;                                                \
-        const bool live = c < g_nchk;                                                           \
+#define TRD_LOAD1(XB)                                                                           \
         const bool fa = 4u * c < g_nt4;                                                         \
         const uint32_t *src = (fa ? pt : pn) + 4u * c;                                          \
         const int lim = live ? (int)(fa ? g_nt : g_nt4 + g_nn) - (int)(4u * c) : 0;             \
@@ -2181,7 +2178,12 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
         } else if (live) {                                                                      \
             const u32x4_a4 q4 = *reinterpret_cast<const u32x4_a4 *>(src);                       \
             XB[u][0] = q4.x; XB[u][1] = q4.y; XB[u][2] = q4.z; XB[u][3] = q4.w;                 \
-        }                                                                                       \
+        }
+#define TRD_LOAD(XB, KB)                                                                        \
+    _Pragma("unroll") for (uint32_t u = 0; u < TRD_P; ++u) {                                    \
+        const uint32_t c = ((KB) + u) * TGD + j;                                                \
+        const bool live = c < g_nchk;                                                           \
+        TRD_LOAD1(XB)                                                                           \
     }
             auto pr = [&](const uint32_t (&xb)[TRD_P][4], uint32_t kb) {
 #pragma unroll
@@ -2220,6 +2222,7 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
                 pr(xb, kb);
             }
 #undef TRD_LOAD
+#undef TRD_LOAD1
             t02 = trd_gsum(t02);
             t13 = trd_gsum(t13);
             n02 = trd_gsum(n02);
