@@ -1541,7 +1541,6 @@ __device__ __forceinline__ void ln_block(const ss_score_args &a, uint32_t s, boo
  * contiguous bytes of each of 64 / TG sites.  (Lane per site, every load
  * instruction touched 64 lines: the texture address and data units were busy
  * 83% / 94% of the kernel's cycles at C4) */
-#define TG 8u                        /* lanes per site in the count pass */
 #ifndef TRI_P
 #define TRI_P 4u                     /* chunk load instructions in flight per round */
 #endif
@@ -1595,13 +1594,14 @@ __device__ __forceinline__ uint32_t tri_chunk(const uint2 *lut, const uint32_t (
     return fl;
 }
 
-/* sum over the TG = 8 lanes of a site's group (DPP: quad_perm xor 1, xor 2,
- * then row_half_mirror, which pairs lane i with 7 - i of the other quad) */
-__device__ __forceinline__ uint32_t tri_gsum(uint32_t v)
+/* sum over the TG = 4 or 8 lanes of a site's group (DPP: quad_perm xor 1,
+ * xor 2, then for 8 row_half_mirror, which pairs lane i with 7 - i of the
+ * other quad) */
+__device__ __forceinline__ uint32_t tri_gsum(uint32_t lg, uint32_t v)
 {
     v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);    /* quad_perm [1,0,3,2] */
     v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);    /* quad_perm [2,3,0,1] */
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);   /* row_half_mirror */
+    if (lg == 3u) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);   /* row_half_mirror */
     return v;
 }
 
@@ -1777,7 +1777,8 @@ __device__ __forceinline__ bool ln_near_eval(const float (&es)[4], const float (
  *     and the site scores 255 (:156).
  * Returns true when it wrote the site's score. */
 __device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *lut, const double *fk, TriLds &T,
-                                          uint32_t lane, uint32_t s, bool insite, uint32_t end_t, uint32_t end_n)
+                                          uint32_t lane, uint32_t s, bool insite, uint32_t end_t, uint32_t end_n,
+                                          uint32_t lg)
 {
     uint32_t ot = 0, ot1 = 0, on = 0, on1 = 0, refc = 'N';
     if (insite) {
@@ -1808,12 +1809,13 @@ __device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *l
                                        end_t < 4u || end_n < 4u);
         /* each round: TG lanes per site (group g = lane / TG takes site
          * round * 64 / TG + g), the site's description by ds_bpermute */
+        const uint32_t TG = 1u << lg;                     /* lanes per site: 4 or 8 (wave-uniform) */
         const uint32_t j = lane & (TG - 1u);
         const uint32_t pk = cand ? (nt | nn << 8 | ref16 << 16) : 0u;    /* nt, nn <= 128 */
         /* TG rounds of 64 / TG sites each */
 #pragma unroll 1
         for (uint32_t r = 0; r < TG; ++r) {
-            const uint32_t site = r * (64u / TG) + lane / TG;
+            const uint32_t site = r << (6u - lg) | lane >> lg;
             const int sa = (int)(site << 2);
             const uint32_t g_pk = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)pk);
             const uint32_t g_ot = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)ot);
@@ -1821,7 +1823,7 @@ __device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *l
             const uint32_t g_nt = g_pk & 0xffu, g_nn = (g_pk >> 8) & 0xffu, g_ref16 = (g_pk >> 16) & 0xfu;
             const uint32_t g_nt4 = (g_nt + 3u) & ~3u;
             const uint32_t g_nchk = g_pk ? (g_nt4 + g_nn + 3u) >> 2 : 0u;    /* the site's chunks (0: not a candidate) */
-            const uint32_t K = wave_max((g_nchk + TG - 1u) / TG);
+            const uint32_t K = wave_max((g_nchk + TG - 1u) >> lg);
             if (K == 0u) continue;
             const uint32_t la = ln_lut_row(1u + g_ref16), lb = ln_lut_row(17u + g_ref16);
             const uint32_t *pt = a.reads_t + g_ot, *pn = a.reads_n + g_on - g_nt4;
@@ -1872,9 +1874,9 @@ __device__ __forceinline__ bool tri_block(const ss_score_args &a, const uint2 *l
                 }
             }
             }
-            cnt_a = tri_gsum(cnt_a);
-            cnt_t = tri_gsum(cnt_t);
-            c24 = tri_gsum(c24);
+            cnt_a = tri_gsum(lg, cnt_a);
+            cnt_t = tri_gsum(lg, cnt_t);
+            c24 = tri_gsum(lg, c24);
             if (j == 0u) {
                 T.cnt_t[site] = cnt_a;
                 T.cnt_n[site] = cnt_t - cnt_a;
@@ -1982,18 +1984,21 @@ void ss_score_triage(ss_score_args a)
         const uint32_t s = blk * 64u + lane;
         const bool insite = s < n_sites;
         /* the block's reads from its offsets (scalar loads) */
-        bool shallow;
+        bool shallow, narrow;
         {
             const ss_score_args &k = kernarg_args();
             const uint32_t s0 = blk * 64u, s1 = min(s0 + 64u, n_sites);
             const uint32_t breads = (k.off_t[s1] - k.off_t[s0]) + (k.off_n[s1] - k.off_n[s0]);
             shallow = breads <= SS_EARLY_MAX_READS * (s1 - s0);
+            narrow = breads <= (SS_EARLY_MAX_READS / 2u) * (s1 - s0);
         }
         const ss_score_args &k = kernarg_args();
         if (shallow) {
             /* every lane of the wave (tri_block's DPP / ballot / bpermute
-             * exchanges read all 64 lanes; it handles lanes past the batch) */
-            const bool d = tri_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n);
+             * exchanges read all 64 lanes; it handles lanes past the batch).
+             * Up to 128 mean reads per site 4 lanes per site (16 sites per
+             * round: C4 +6%, C2 +12%), past that 8 (C3: 4 lanes -1.5%) */
+            const bool d = tri_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n, narrow ? 2u : 3u);
             const bool need = insite && !d;
             const uint64_t m = __ballot(need);
             if (m) {                                     /* few at 30x .. 100x: one atomic per wave */

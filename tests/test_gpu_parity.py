@@ -524,6 +524,30 @@ def test_near_exit_deep_parity(pkg, oracle, opts):
         assert_parity(pkg, oracle, b, opts)
 
 
+@pytest.mark.parametrize("lt,ln,deep,left", [(60, 30, False, 0.01), (100, 60, False, 0.04), (500, 500, True, 0.001),
+                                              (1200, 1000, True, 0.04)])
+def test_triage_routing(pkg, lt, ln, deep, left):
+    """Where the device path sends a synthetic batch's sites (the performance
+    contract of DESIGN.md 4.0-4.0.1, not a parity check): the triage kernels
+    decide all but a few per thousand, the deep triage takes exactly the
+    blocks past 128 mean reads per sample, and what is left reaches the main
+    kernel's list and, past 128 reads, the group or deep kernel."""
+    import torch
+    n = 1 << 16
+    dev = torch.device("cuda", 0)
+    with pkg.Context(pkg.Params.default(), device=0) as ctx:
+        d = ctx.synth_device(pkg.Synth.default(lt, ln, seed=5), 0, n, device=dev)
+        score = torch.empty(n, dtype=torch.int32, device=dev)
+        ctx.score_device(d["ref"], d["off_tumor"], d["off_normal"], d["reads_tumor"], d["reads_normal"], score=score)
+        torch.cuda.synchronize(dev)
+        ctx.check()
+        r = ctx._route_counts()
+    assert r["deep_triage_blocks"] == (n // 64 if deep else 0), r
+    assert r["main_sites"] <= left * n, r
+    assert r["group_sites"] + r["deep_sites"] <= r["main_sites"], r
+    assert (score.cpu().numpy() == 255).mean() > 0.9
+
+
 @pytest.mark.parametrize("shift", [1, 2, 3])
 def test_misaligned_read_arrays(pkg, oracle, shift):
     """Device-resident read arrays that start 4, 8 or 12 bytes past a 16-byte

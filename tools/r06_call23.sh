@@ -9,7 +9,7 @@ timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --t
     --durations=8 -k "${K:-near_exit or synthetic_parity or deep_parity or group}" > "$O/pytest.log" 2>&1; rc=$?
 tail -12 "$O/pytest.log"
 [ $rc -eq 0 ] || exit $rc
-for cfg in "c5 500 500 1048576" "d1200 1200 1000 262144" "c4 60 30 67108864"; do
+for cfg in "c5 500 500 1048576" "d1200 1200 1000 262144" "c4 60 30 67108864" "c2 30 30 67108864" "c3 100 60 33554432"; do
   set -- $cfg
   timeout -k 10 300 python3 bench.py --workload shard --no-cpu --no-host-fed --steps 10 --warmup 2 \
       --lt "$2" --ln "$3" --sites "$4" > "$O/bench_$1.json" 2> "$O/bench_$1.err" || { tail -5 "$O/bench_$1.err"; exit 1; }

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 6: the full GPU suite and smoke() on the current tree, then the shard
+# bench lines (C5, 1200x/1000x, C4, C2, C3).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r06c35
+mkdir -p "$O"
+cd "$R"
+timeout -k 10 800 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread --durations=15 \
+    > "$O/pytest_gpu.log" 2>&1; rc=$?
+tail -5 "$O/pytest_gpu.log"
+[ $rc -eq 0 ] || { grep -E "FAILED|Error" "$O/pytest_gpu.log" | head; exit $rc; }
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1; rc=$?
+tail -2 "$O/smoke.log"
+[ $rc -eq 0 ] || exit $rc
+for cfg in "c5 500 500 1048576" "d1200 1200 1000 262144" "c4 60 30 67108864" "c2 30 30 67108864" "c3 100 60 33554432"; do
+  set -- $cfg
+  timeout -k 10 200 python3 bench.py --workload shard --no-cpu --no-host-fed --steps 10 --warmup 2 \
+      --lt "$2" --ln "$3" --sites "$4" > "$O/bench_$1.json" 2> "$O/bench_$1.err" || { tail -5 "$O/bench_$1.err"; exit 1; }
+  echo "$1 $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print('%.3e sites/s' % d['value'], r['avg_ms_by_kernel'], 'frac', r['frac'], 'traffic/alg', r.get('traffic_over_algorithmic'), r.get('traffic_bytes_per_site'), r.get('valu',{}).get('insts_per_site'))" "$O/bench_$1.json")"
+done
