@@ -531,7 +531,7 @@ static int ensure_deep_cap(ss_ctx_t *c, uint64_t n_sites, hipStream_t s)
     if (cap < n_sites) return SS_E_INVAL;
     dev_release(c, *(void **)&c->d_deep_list, false);
     c->deep_cap = 0;
-    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 5 * cap * sizeof(uint32_t), s)) return rc;
+    if (int rc = dev_alloc(c, (void **)&c->d_deep_list, 6 * cap * sizeof(uint32_t), s)) return rc;
     c->deep_cap = (uint32_t)cap;
     return SS_OK;
 }
@@ -591,7 +591,7 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     /* counters: deep2, listed segments and entries, the group and deep
      * kernels' next chunks, deep3, the triage list (err is sticky until
      * ss_ctx_check) */
-    HIPCHK(hipMemsetAsync(c->d_counters + 4, 0, 8 * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(c->d_counters + 4, 0, 9 * sizeof(uint32_t), s));
     if (o->n_calls) HIPCHK(hipMemsetAsync(o->n_calls, 0, sizeof(uint32_t), s));
     ss_score_args a;
     memset(&a, 0, sizeof(a));
@@ -628,6 +628,8 @@ extern "C" int ss_score_batch_device(ss_ctx_t *c, const ss_batch_t *b, const ss_
     a.tri_count = c->d_counters + 11;
     a.dtri_list = c->d_deep_list + 4 * (size_t)c->deep_cap;
     a.dtri_count = c->d_counters + 4;
+    a.dsite_list = c->d_deep_list + 5 * (size_t)c->deep_cap;
+    a.dsite_count = c->d_counters + 12;
     a.err = c->d_counters + 2;
     a.m.tab = c->d_tab;
     a.m.q_r_int = c->hm.q_r_int;

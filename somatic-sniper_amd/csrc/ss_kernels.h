@@ -89,6 +89,8 @@ struct ss_score_args {
     uint32_t  *dtri_list;     /* the triage kernel's 64-site blocks past SS_EARLY_MAX_READS mean reads (block
                                  indices), for the deep triage kernel */
     uint32_t  *dtri_count;
+    uint32_t  *dsite_list;    /* the triage kernel's undecided sites, for the deep triage's wider test */
+    uint32_t  *dsite_count;
     uint32_t  *err;           /* sticky error bits, see SS_KERR_* */
     uint8_t   *grp_rec;       /* the group kernel's fold records: SS_GRP_REC_BYTES per wave */
     ss_dev_model m;

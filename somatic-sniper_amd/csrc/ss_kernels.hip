@@ -1999,15 +1999,17 @@ void ss_score_triage(ss_score_args a)
              * Up to 128 mean reads per site 4 lanes per site (16 sites per
              * round: C4 +6%, C2 +12%), past that 8 (C3: 4 lanes -1.5%) */
             const bool d = tri_block(kernarg_args(), lut, fk, TL[wv], lane, s, insite, end_t, end_n, narrow ? 2u : 3u);
+            /* an undecided site (more than 3 off-reference reads, a sample past
+             * 128 reads, or a real candidate) gets the deep triage's wider test */
             const bool need = insite && !d;
             const uint64_t m = __ballot(need);
             if (m) {                                     /* few at 30x .. 100x: one atomic per wave */
                 const uint32_t first = (uint32_t)__builtin_ctzll(m);
                 uint32_t base = 0;
-                if (lane == first) base = atomicAdd(k.tri_count, (uint32_t)__popcll(m));
+                if (lane == first) base = atomicAdd(k.dsite_count, (uint32_t)__popcll(m));
                 base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
-                if (need) k.tri_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
+                if (need) k.dsite_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
             }
         } else {
             stage_push(hb, nb, lane == 0u, blk, k.dtri_count, k.dtri_list, lane);
@@ -2291,8 +2293,10 @@ __device__ __forceinline__ bool trd_block(const ss_score_args &a, const uint2 *l
 }
 
 /* Deep triage kernel: the blocks the triage kernel found past
- * SS_EARLY_MAX_READS mean reads (a wave per listed block, lane = site);
- * undecided sites go on to the main kernel's list. */
+ * SS_EARLY_MAX_READS mean reads (a wave per listed block, lane = site), then
+ * the sites the triage kernel's narrower test left (64 per wave: up to 16
+ * off-reference reads per sample here, 3 there); undecided sites go on to the
+ * main kernel's list. */
 __global__ __launch_bounds__(SS_TRIAGE_DEEP_BLOCK) void ss_score_triage_deep(ss_score_args a)
 {
     __shared__ double fk[LN_FK_ZERO + 1];
@@ -2300,7 +2304,9 @@ __global__ __launch_bounds__(SS_TRIAGE_DEEP_BLOCK) void ss_score_triage_deep(ss_
     __shared__ TriLdsD TL[SS_TRIAGE_DEEP_BLOCK / 64];
     const uint32_t n_sites = (uint32_t)a.n_sites;
     const uint32_t nlisted = min(*a.dtri_count, (n_sites + 63u) / 64u);
-    if (blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) >= nlisted) return;
+    const uint32_t nsl = min(*a.dsite_count, n_sites);
+    const uint32_t nitems = nlisted + (nsl + 63u) / 64u;        /* listed blocks, then groups of 64 listed sites */
+    if (blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) >= nitems) return;
     for (uint32_t i = threadIdx.x; i <= LN_FK_ZERO; i += blockDim.x) fk[i] = i < LN_FK_LIVE ? ss_tab_fk(a.m)[i] : 0.0;
     ln_lut_build(lut);
     __syncthreads();
@@ -2309,10 +2315,17 @@ __global__ __launch_bounds__(SS_TRIAGE_DEEP_BLOCK) void ss_score_triage_deep(ss_
     const uint32_t nwaves = gridDim.x * (SS_TRIAGE_DEEP_BLOCK / 64);
     const uint32_t end_t = a.off_t[n_sites], end_n = a.off_n[n_sites];
     uint32_t ns = 0, hs = 0;
-    for (uint32_t i = blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) + wv; i < nlisted; i += nwaves) {
-        const uint32_t blk = kernarg_args().dtri_list[i];
-        const uint32_t s = blk * 64u + lane;
-        const bool insite = s < n_sites;
+    for (uint32_t i = blockIdx.x * (SS_TRIAGE_DEEP_BLOCK / 64) + wv; i < nitems; i += nwaves) {
+        uint32_t s;
+        bool insite;
+        if (i < nlisted) {                               /* wave-uniform */
+            s = kernarg_args().dtri_list[i] * 64u + lane;
+            insite = s < n_sites;
+        } else {
+            const uint32_t e = (i - nlisted) * 64u + lane;
+            insite = e < nsl;
+            s = insite ? kernarg_args().dsite_list[e] : 0u;
+        }
         const bool d = trd_block(kernarg_args(), lut, fk, TL[wv], lane, insite ? s : 0u, insite, end_t, end_n);
         const ss_score_args &k = kernarg_args();
         stage_push(hs, ns, insite && !d, s, k.tri_count, k.tri_list, lane);

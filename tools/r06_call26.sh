@@ -2,7 +2,7 @@
 # Round 6: per-kernel times at C5 and 1200x/1000x after the deep triage.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r06c34
+O=$R/gpurun_out/r06c36
 mkdir -p "$O"
 cd "$R"
 export TMPDIR=/tmp
